@@ -1,0 +1,192 @@
+// eg_bignum.hpp — CDNA4 (gfx950) device core for 4096-bit Montgomery arithmetic.
+//
+// Replaces the upstream GroupContext / ElementModP arithmetic reached through
+// KUtils.productionGroup() (src/main/java/electionguard/util/KUtils.java:10-12):
+// ElementModP.times / multP and the powP built from them.  Results are the unique
+// integers mod p, i.e. identical to java.math.BigInteger.modPow / multiply+mod.
+//
+// Representation (MI355X-first):
+//   * radix 2^27, N = 152 limbs (4104 bits), Montgomery R = 2^4104 > 4p, so the
+//     CIOS loop never needs a final subtraction (values stay < 2p between ops);
+//   * 27-bit limbs let every column accumulate in a 64-bit register with ONE
+//     v_mad_u64_u32 per limb product (2N products x 2^54 < 2^63 — no carry-out
+//     handling inside the loop); the gfx950 microbenchmark (profiles/r01_ubench_isa.txt)
+//     shows v_mad_u64_u32 issues at the same rate as a 32-bit add, so the cost of a
+//     Montgomery multiply is its instruction count;
+//   * one element is owned by a group of T = EG_T consecutive lanes (a DPP quad or
+//     half-row); lane l of the group holds limbs [l*L, l*L+L), L = N/T, in VGPRs;
+//   * the multiplier operand y is read from a per-group LDS slot (group-uniform
+//     broadcast read), the modulus limbs p live in VGPRs, the accumulator t in
+//     L 64-bit VGPR pairs whose register names rotate by one per step (unrolled L
+//     steps), so the CIOS "shift by one limb" costs one DPP row_shl:1 per step.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef EG_T
+#define EG_T 8
+#endif
+
+namespace eg {
+
+constexpr int kLimbBits = 27;
+constexpr uint32_t kMask = (1u << kLimbBits) - 1u;
+constexpr int kN = 152;               // limbs per element
+constexpr int kT = EG_T;              // lanes per element
+constexpr int kL = kN / kT;           // limbs per lane
+constexpr int kLP = (kL + 3) & ~3;    // padded limbs per lane (16-B aligned lane blocks)
+constexpr int kW = kT * kLP;          // words per device element (160 for T=4 and T=8)
+constexpr int kYStride = kW + 4;      // LDS words per group slot (bank spread)
+constexpr int kWave = 64;
+constexpr int kGroupsPerWave = kWave / kT;
+static_assert(kN % kT == 0, "limbs must split evenly over the group");
+static_assert(kT == 4 || kT == 8, "EG_T must be 4 or 8");
+static_assert(kW == 160, "device element format is 160 words");
+
+// Device constants of one group context (filled by the host, eg_capi.hip).
+struct MontConsts {
+  uint32_t p[kW];      // modulus limbs, device element format (radix 2^27)
+  uint32_t r2[kW];     // R^2 mod p (normal form)        -> to-Montgomery multiplier
+  uint32_t one[kW];    // R mod p (Montgomery form of 1)
+  uint32_t unit[kW];   // the integer 1 (limb 0 = 1)      -> from-Montgomery multiplier
+  uint32_t pw[128];    // p as 128 little-endian 32-bit words (final compare / subtract)
+  uint32_t n0;         // -p^-1 mod 2^27
+  uint32_t friendly;   // n0 == 1 (p = -1 mod 2^27): EG production group
+};
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ int glane() { return lane_id() & (kT - 1); }   // lane within element group
+__device__ __forceinline__ int gslot() { return lane_id() / kT; }        // group index within wave
+
+// Broadcast group-lane 0's value to the whole group.
+__device__ __forceinline__ uint32_t bcast_g0(uint32_t v) {
+  uint32_t a = __builtin_amdgcn_mov_dpp(v, 0x00 /*quad_perm [0,0,0,0]*/, 0xF, 0xF, false);
+  if constexpr (kT == 8) {
+    // lanes 4-7 / 12-15 of every row take the value 4 lanes below (the group's lane 0)
+    a = __builtin_amdgcn_update_dpp(a, a, 0x114 /*row_shr:4*/, 0xF, 0xA, false);
+  }
+  return a;
+}
+
+// value from lane+1 within the DPP row (0 at the row end)
+__device__ __forceinline__ uint32_t from_next(uint32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x101 /*row_shl:1*/, 0xF, 0xF, true);
+}
+// value from lane-1 within the DPP row (0 at the row start)
+__device__ __forceinline__ uint32_t from_prev(uint32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x111 /*row_shr:1*/, 0xF, 0xF, true);
+}
+
+// Montgomery multiply  x <- x * y * R^-1 mod p  (result < 2p, limbs < 2^27 + 2^11).
+//   x : this lane's L limbs (in/out), any value < 2p, limbs <= 2^27 + 2^11
+//   y : the group's LDS slot (kW words, device element format), value < 2p
+//   p : this lane's L modulus limbs
+// CIOS, one radix-2^27 digit of y per step; 2L v_mad_u64_u32 + ~5 VALU per step.
+template <bool FRIENDLY>
+__device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
+                                         const uint32_t (&p)[kL], uint32_t n0, uint32_t mask) {
+  uint64_t acc[kL];
+#pragma unroll
+  for (int j = 0; j < kL; ++j) acc[j] = 0;
+
+#pragma unroll 1
+  for (int s = 0; s < kT; ++s) {
+    const uint32_t* ys = y + s * kLP;
+#pragma unroll
+    for (int r = 0; r < kL; ++r) {
+      const uint32_t yi = ys[r];
+      // t += x * y_i     (logical position j lives in register (j + r) % L)
+#pragma unroll
+      for (int j = 0; j < kL; ++j) {
+        uint64_t& A = acc[(j + r) % kL];
+        A = (uint64_t)x[j] * yi + A;
+      }
+      // quotient digit from the group's lowest limb
+      uint32_t t0 = (uint32_t)acc[r % kL];
+      if constexpr (!FRIENDLY) t0 *= n0;
+      const uint32_t m = bcast_g0(t0) & mask;
+      // t += m * p
+#pragma unroll
+      for (int j = 0; j < kL; ++j) {
+        uint64_t& A = acc[(j + r) % kL];
+        A = (uint64_t)p[j] * m + A;
+      }
+      // split the lowest column: carry stays in this lane (next position),
+      // low 27 bits shift into lane-1's top position (0 for the group's lane 0)
+      uint64_t& A0 = acc[r % kL];
+      acc[(r + 1) % kL] += A0 >> kLimbBits;
+      A0 = (uint64_t)(from_next((uint32_t)A0) & mask);
+    }
+  }
+  // two parallel carry passes -> limbs < 2^27 + 2^11 (enough headroom for the next op)
+  uint64_t d[kL];
+  {
+    uint64_t c_in = ((uint64_t)from_prev((uint32_t)(acc[kL - 1] >> kLimbBits)) |
+                     ((uint64_t)from_prev((uint32_t)(acc[kL - 1] >> (kLimbBits + 32))) << 32));
+#pragma unroll
+    for (int j = 0; j < kL; ++j) {
+      const uint64_t c = (j == 0) ? c_in : (acc[j - 1] >> kLimbBits);
+      d[j] = (uint64_t)((uint32_t)acc[j] & mask) + c;
+    }
+  }
+  {
+    const uint32_t c_in = from_prev((uint32_t)(d[kL - 1] >> kLimbBits));
+#pragma unroll
+    for (int j = 0; j < kL; ++j) {
+      const uint32_t c = (j == 0) ? c_in : (uint32_t)(d[j - 1] >> kLimbBits);
+      x[j] = ((uint32_t)d[j] & mask) + c;
+    }
+  }
+}
+
+// Generic dispatch on the friendliness of p (wave-uniform).
+__device__ __forceinline__ void mmul(uint32_t (&x)[kL], const uint32_t* y, const uint32_t (&p)[kL],
+                                     uint32_t n0, uint32_t mask, bool friendly) {
+  if (friendly) mont_mul<true>(x, y, p, n0, mask);
+  else mont_mul<false>(x, y, p, n0, mask);
+}
+
+// ---- element I/O between VGPRs, LDS slots and the device element format ----
+
+__device__ __forceinline__ void load_elem(uint32_t (&x)[kL], const uint32_t* __restrict__ src) {
+  const uint32_t* s = src + glane() * kLP;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) x[j] = s[j];
+}
+
+__device__ __forceinline__ void store_elem(uint32_t* __restrict__ dst, const uint32_t (&x)[kL]) {
+  uint32_t* s = dst + glane() * kLP;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) s[j] = x[j];
+#pragma unroll
+  for (int j = kL; j < kLP; ++j) s[j] = 0;
+}
+
+// copy a device element (global) into the group's LDS slot, each lane its block
+__device__ __forceinline__ void elem_to_lds(uint32_t* __restrict__ slot, const uint32_t* __restrict__ src) {
+  const int o = glane() * kLP;
+  static_assert(kLP % 4 == 0, "");
+#pragma unroll
+  for (int j = 0; j < kLP; j += 4) {
+    *reinterpret_cast<uint4*>(slot + o + j) = *reinterpret_cast<const uint4*>(src + o + j);
+  }
+}
+
+__device__ __forceinline__ void regs_to_lds(uint32_t* __restrict__ slot, const uint32_t (&x)[kL]) {
+  uint32_t* s = slot + glane() * kLP;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) s[j] = x[j];
+}
+
+// ---- conversion between 512-byte big-endian (common.proto:6-10) and limbs ----
+
+// Read bits [b, b+27) of a little-endian word array of 128 words (zero above 4096).
+__device__ __forceinline__ uint32_t bits27(const uint32_t* __restrict__ w, int b) {
+  const int wi = b >> 5, sh = b & 31;
+  const uint32_t lo = (wi < 128) ? w[wi] : 0u;
+  const uint32_t hi = (wi + 1 < 128) ? w[wi + 1] : 0u;
+  const uint64_t v = ((uint64_t)hi << 32) | lo;
+  return (uint32_t)(v >> sh) & kMask;
+}
+
+}  // namespace eg

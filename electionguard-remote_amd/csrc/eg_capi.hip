@@ -1,0 +1,601 @@
+// eg_capi.hip — host side of libeg_hip.so: the C ABI declared in include/eg_hip.h.
+//
+// Reference interfaces replaced (file:line under /root/reference):
+//   GroupContext construction  KUtils.productionGroup            KUtils.java:10-12
+//   element wire import/export ConvertCommonProto                ConvertCommonProto.java:41-57,111-121
+//   batchEncryption / runAccumulateBallots / Verifier             RunRemoteWorkflowTest.java:140-141,151,179-182
+//   DecryptingTrusteeIF.directDecrypt / compensatedDecrypt       RunRemoteDecryptingTrustee.java:189-193,227-232
+// The arithmetic itself is upstream (electionguard-kotlin-multiplatform-jvm, not in
+// the container); see DESIGN.md for the restated algorithms.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#pragma clang diagnostic ignored "-Wunused-result"
+#pragma clang diagnostic ignored "-Wunused-value"
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/eg_hip.h"
+#include "eg_kernels.hpp"
+
+using namespace eg;
+
+// ------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess)                                                           \
+      return fail(EG_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+extern "C" const char* eg_last_error(void) { return g_err.c_str(); }
+
+extern "C" int eg_version(char* buf, size_t len) {
+  if (!buf || !len) return fail(EG_ERR_ARG, "null buffer");
+  snprintf(buf, len, "eg_hip gfx950 radix2^%d limbs=%d lanes/elem=%d words/elem=%d", kLimbBits, kN, kT, kW);
+  return EG_OK;
+}
+
+// ------------------------------------------------------------------------------
+// host bignum helpers (constants only; 128 little-endian 32-bit words)
+// ------------------------------------------------------------------------------
+using Big = std::vector<uint32_t>;
+
+static Big be_to_words(const uint8_t* be, int nbytes) {
+  Big w((nbytes + 3) / 4, 0);
+  for (int i = 0; i < nbytes; ++i) {
+    const int bit = (nbytes - 1 - i) * 8;
+    w[bit / 32] |= (uint32_t)be[i] << (bit % 32);
+  }
+  return w;
+}
+static bool ge(const Big& a, const Big& b) {
+  for (int i = (int)a.size() - 1; i >= 0; --i)
+    if (a[i] != b[i]) return a[i] > b[i];
+  return true;
+}
+static void sub_in(Big& a, const Big& b) {
+  int64_t c = 0;
+  for (size_t i = 0; i < a.size(); ++i) {
+    c += (int64_t)a[i] - b[i];
+    a[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+// a = 2a mod m  (a < m, m < 2^(32*size))
+static void dbl_mod(Big& a, const Big& m) {
+  uint32_t top = 0;
+  for (size_t i = 0; i < a.size(); ++i) {
+    const uint32_t nt = a[i] >> 31;
+    a[i] = (a[i] << 1) | top;
+    top = nt;
+  }
+  if (top || ge(a, m)) sub_in(a, m);
+}
+// words (LE, 128+) -> device element format (radix 2^27 limbs, padded lane blocks)
+static void words_to_elem(const Big& w, uint32_t* out) {
+  std::memset(out, 0, sizeof(uint32_t) * kW);
+  for (int a = 0; a < kN; ++a) {
+    const int bit = a * kLimbBits;
+    uint64_t v = 0;
+    for (int k = 0; k < 3; ++k) {
+      const int wi = bit / 32 + k;
+      if (wi < (int)w.size()) v |= (uint64_t)w[wi] << (32 * k);
+    }
+    const uint32_t limb = (uint32_t)(v >> (bit % 32)) & kMask;
+    out[(a / kL) * kLP + (a % kL)] = limb;
+  }
+}
+
+// ------------------------------------------------------------------------------
+// context
+// ------------------------------------------------------------------------------
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+struct ProfRec {
+  hipEvent_t a, b;
+  double mm;
+};
+
+struct eg_fixed_base {
+  eg_ctx* ctx = nullptr;
+  uint32_t* d_tab = nullptr;
+  int wbits = 0, nwin = 0;
+  FbTab tab() const { return FbTab{d_tab, (uint32_t)wbits, (uint32_t)nwin}; }
+};
+
+enum Slot {
+  W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_NSLOT
+};
+
+struct eg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  MontConsts h{};
+  MontConsts* d = nullptr;
+  uint8_t p_be[512], q_be[32], g_be[512];
+  uint8_t* d_q = nullptr;
+  uint8_t* d_qbar = nullptr;
+  eg_fixed_base* gtab = nullptr;
+  eg_fixed_base* Ktab = nullptr;
+  DevBuf ws[W_NSLOT];
+  bool timing = false;
+  std::vector<ProfRec> prof;
+  uint8_t K_be[512];
+  std::map<std::string, DevBuf> cache;  // shape-keyed job tables
+};
+static std::vector<ProfRec>& prof_of(eg_ctx* c) { return c->prof; }
+
+static int ws_get(eg_ctx* c, Slot s, size_t bytes, void** out) {
+  DevBuf& b = c->ws[s];
+  if (b.bytes < bytes) {
+    if (b.ptr) HIPCHK(hipFree(b.ptr));
+    b.ptr = nullptr;
+    b.bytes = 0;
+    size_t want = std::max(bytes, (size_t)4096);
+    hipError_t e = hipMalloc(&b.ptr, want);
+    if (e != hipSuccess) return fail(EG_ERR_NOMEM, "hipMalloc workspace " + std::to_string(want) + " B failed");
+    b.bytes = want;
+  }
+  *out = b.ptr;
+  return EG_OK;
+}
+
+// launch the Montgomery-friendly or general instantiation of a kernel template
+#define LAUNCH_F(c, K, grid, ...)                                                              \
+  do {                                                                                        \
+    if ((c)->h.friendly)                                                                      \
+      hipLaunchKernelGGL(K<true>, grid, dim3(kBlock), 0, (c)->stream, __VA_ARGS__);            \
+    else                                                                                      \
+      hipLaunchKernelGGL(K<false>, grid, dim3(kBlock), 0, (c)->stream, __VA_ARGS__);           \
+  } while (0)
+
+static inline unsigned grid_for(size_t groups) { return (unsigned)((groups + kGroupsPerBlock - 1) / kGroupsPerBlock); }
+static inline size_t padded_groups(size_t groups) { return (size_t)grid_for(groups) * kGroupsPerBlock; }
+
+// ---- launch wrappers (ctx stream) ----
+static int launch_import(eg_ctx* c, const uint8_t* d_be, size_t n, uint32_t* d_out, uint8_t* d_ltp) {
+  if (!n) return EG_OK;
+  LAUNCH_F(c, k_import, dim3(grid_for(n)), c->d, d_be, (uint32_t)n, d_out, d_ltp);
+  HIPCHK(hipGetLastError());
+  return EG_OK;
+}
+static int launch_export(eg_ctx* c, const uint32_t* d_in, size_t n, uint8_t* d_be) {
+  if (!n) return EG_OK;
+  LAUNCH_F(c, k_export, dim3(grid_for(n)), c->d, d_in, (uint32_t)n, d_be);
+  HIPCHK(hipGetLastError());
+  return EG_OK;
+}
+
+// Algorithmic Montgomery multiplications of one k_pow job (mirrors the kernel).
+static double pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
+  double mm = S.has_base ? 14.0 : 0.0;
+  for (uint32_t o = 0; o < S.nout; ++o) {
+    bool one = true;
+    if (S.has_base) {
+      mm += (double)(S.exp_bytes * 2 - 1) * 5.0;
+      one = false;
+    }
+    for (uint32_t t = 0; t < S.nfb[o]; ++t) {
+      const FbTab& T = S.tab[o][t] ? f1 : f0;
+      mm += (double)T.nwin - (one ? 1.0 : 0.0);
+      one = false;
+    }
+  }
+  return mm;
+}
+
+
+// Run a homogeneous batch of exponentiation jobs (device job records).
+static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
+                      const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1) {
+  if (!njobs) return EG_OK;
+  uint32_t* scr = nullptr;
+  const size_t per = S.has_base ? (size_t)16 * kW * 4 : 4;
+  // bound the per-launch scratch (table of 16 powers per job)
+  const size_t max_jobs = (size_t)1 << 18;
+  const double mm_job = pow_job_mm(S, f0, f1);
+  for (size_t off = 0; off < njobs; off += max_jobs) {
+    const size_t nj = std::min(max_jobs, njobs - off);
+    int rc = ws_get(c, W_SCR, padded_groups(nj) * per, (void**)&scr);
+    if (rc) return rc;
+    ProfRec pr{nullptr, nullptr, mm_job * (double)nj};
+    if (c->timing) {
+      HIPCHK(hipEventCreate(&pr.a));
+      HIPCHK(hipEventCreate(&pr.b));
+      HIPCHK(hipEventRecord(pr.a, c->stream));
+    }
+    LAUNCH_F(c, k_pow, dim3(grid_for(nj)), c->d, S, d_jobs + off * kJobWords,
+                       (uint32_t)nj, d_elems, d_scal, d_out, scr, f0, f1);
+    HIPCHK(hipGetLastError());
+    if (c->timing) {
+      HIPCHK(hipEventRecord(pr.b, c->stream));
+      prof_of(c).push_back(pr);
+    }
+  }
+  return EG_OK;
+}
+
+// Product reduction of `groups` groups of `len` device elements (group layout gm,
+// element stride `stride`); result -> d_out[g].  Fully asynchronous.
+static int run_prod(eg_ctx* c, const uint32_t* d_in, GroupMap gm, size_t groups, size_t len, size_t stride,
+                    uint32_t* d_out) {
+  if (!groups) return EG_OK;
+  if (len == 0) return fail(EG_ERR_ARG, "empty product");
+  const uint32_t chunk = 32;
+  const size_t maxpart = groups * ((len + chunk - 1) / chunk);
+  uint32_t* tmp = nullptr;
+  int rc = ws_get(c, W_TMP, std::max<size_t>(1, maxpart) * kW * 4 * 2, (void**)&tmp);
+  if (rc) return rc;
+  uint32_t* ping[2] = {tmp, tmp + maxpart * kW};
+  size_t cur_len = len, cur_stride = stride;
+  const uint32_t* src = d_in;
+  int pi = 0;
+  while (true) {
+    const uint32_t nchunk = (uint32_t)((cur_len + chunk - 1) / chunk);
+    const uint32_t ch = nchunk == 1 ? (uint32_t)cur_len : chunk;
+    uint32_t* dst = (nchunk == 1) ? d_out : ping[pi];
+    const size_t njobs = groups * nchunk;
+    LAUNCH_F(c, k_prod, dim3(grid_for(njobs)), c->d, src, gm, (uint32_t)groups,
+                       (uint32_t)cur_len, (uint32_t)cur_stride, ch, nchunk, dst);
+    HIPCHK(hipGetLastError());
+    if (nchunk == 1) break;
+    // next round: group g's partials are contiguous at g*nchunk
+    gm = GroupMap{1, 1, 0, 0, nchunk};
+    src = dst;
+    cur_len = nchunk;
+    cur_stride = 1;
+    pi ^= 1;
+  }
+  return EG_OK;
+}
+
+// ---- fixed-base table build ----
+static int build_fb(eg_ctx* c, const uint32_t* d_base_mont, int wbits, eg_fixed_base* fb) {
+  const int nwin = (256 + wbits - 1) / wbits;
+  const size_t entries = (size_t)nwin << wbits;
+  HIPCHK(hipMalloc(&fb->d_tab, entries * kW * 4));
+  fb->wbits = wbits;
+  fb->nwin = nwin;
+  // powers base^(2^j), j < nwin*wbits
+  uint32_t* P = nullptr;
+  const int npow = nwin * wbits;
+  HIPCHK(hipMalloc(&P, (size_t)npow * kW * 4));
+  LAUNCH_F(c, k_sqr_chain, dim3(1), c->d, d_base_mont, (uint32_t)npow, P);
+  HIPCHK(hipGetLastError());
+  // entries (k, 0) = one, (k, 2^a) = P[k*wbits + a]
+  for (int k = 0; k < nwin; ++k) {
+    uint32_t* row = fb->d_tab + ((size_t)k << wbits) * kW;
+    HIPCHK(hipMemcpyAsync(row, c->d->one, kW * 4, hipMemcpyDeviceToDevice, c->stream));
+    for (int a = 0; a < wbits; ++a)
+      HIPCHK(hipMemcpyAsync(row + ((size_t)1 << a) * kW, P + (size_t)(k * wbits + a) * kW, kW * 4,
+                            hipMemcpyDeviceToDevice, c->stream));
+  }
+  for (int a = 1; a < wbits; ++a) {
+    const size_t njobs = (size_t)nwin * (((size_t)1 << a) - 1);
+    LAUNCH_F(c, k_fb_level, dim3(grid_for(njobs)), c->d, fb->d_tab,
+                       (uint32_t)wbits, (uint32_t)nwin, (uint32_t)a);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipFree(P));
+  return EG_OK;
+}
+
+static int import_one(eg_ctx* c, const uint8_t be[512], uint32_t** d_mont_out) {
+  uint8_t* d_be = nullptr;
+  uint32_t* d_m = nullptr;
+  HIPCHK(hipMalloc(&d_be, 512));
+  HIPCHK(hipMalloc(&d_m, kW * 4));
+  HIPCHK(hipMemcpyAsync(d_be, be, 512, hipMemcpyHostToDevice, c->stream));
+  int rc = launch_import(c, d_be, 1, d_m, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipFree(d_be));
+  *d_mont_out = d_m;
+  return EG_OK;
+}
+
+static int fb_create_locked(eg_ctx* c, const uint8_t base_be[512], int wbits, eg_fixed_base** out) {
+  if (!(wbits == 4 || wbits == 8 || wbits == 11 || wbits == 12 || wbits == 16))
+    return fail(EG_ERR_ARG, "window_bits must be 4, 8, 11, 12 or 16");
+  uint32_t* d_m = nullptr;
+  int rc = import_one(c, base_be, &d_m);
+  if (rc) return rc;
+  auto* fb = new eg_fixed_base();
+  fb->ctx = c;
+  rc = build_fb(c, d_m, wbits, fb);
+  hipFree(d_m);
+  if (rc) {
+    delete fb;
+    return rc;
+  }
+  *out = fb;
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], const uint8_t g_be[512], int device,
+                             eg_ctx** out) {
+  if (!p_be || !q_be || !g_be || !out) return fail(EG_ERR_ARG, "null argument");
+  *out = nullptr;
+  const Big p = be_to_words(p_be, 512);
+  if ((p[0] & 1) == 0) return fail(EG_ERR_MODULUS, "p must be odd");
+  if ((p[127] >> 31) == 0) return fail(EG_ERR_MODULUS, "p must be a 4096-bit modulus (top bit set)");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(EG_ERR_ARG, "bad device ordinal " + std::to_string(device));
+  HIPCHK(hipSetDevice(device));
+  auto* c = new eg_ctx();
+  c->device = device;
+  std::memcpy(c->p_be, p_be, 512);
+  std::memcpy(c->q_be, q_be, 32);
+  std::memcpy(c->g_be, g_be, 512);
+  // Montgomery constants, R = 2^(27*152)
+  Big P1 = p;
+  P1.push_back(0);  // room for doubling
+  Big r(129, 0);
+  r[0] = 1;
+  for (int i = 0; i < kN * kLimbBits; ++i) dbl_mod(r, P1);  // R mod p
+  Big r2 = r;
+  for (int i = 0; i < kN * kLimbBits; ++i) dbl_mod(r2, P1);  // R^2 mod p
+  words_to_elem(p, c->h.p);
+  words_to_elem(r2, c->h.r2);
+  words_to_elem(r, c->h.one);
+  Big unit(128, 0);
+  unit[0] = 1;
+  words_to_elem(unit, c->h.unit);
+  for (int i = 0; i < 128; ++i) c->h.pw[i] = p[i];
+  // n0 = -p^-1 mod 2^27 (Newton on 32 bits)
+  uint32_t inv = 1;
+  for (int i = 0; i < 6; ++i) inv *= 2u - p[0] * inv;
+  c->h.n0 = (0u - inv) & kMask;
+  c->h.friendly = c->h.n0 == 1 ? 1u : 0u;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(EG_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  HIPCHK(hipMalloc(&c->d, sizeof(MontConsts)));
+  HIPCHK(hipMemcpy(c->d, &c->h, sizeof(MontConsts), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&c->d_q, 32));
+  HIPCHK(hipMemcpy(c->d_q, q_be, 32, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&c->d_qbar, 32));
+  std::lock_guard<std::mutex> lk(c->mu);
+  int rc = fb_create_locked(c, g_be, 8, &c->gtab);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return EG_OK;
+}
+
+extern "C" int eg_fixed_base_destroy(eg_fixed_base* fb) {
+  if (!fb) return EG_OK;
+  if (fb->d_tab) hipFree(fb->d_tab);
+  delete fb;
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_destroy(eg_ctx* c) {
+  if (!c) return EG_OK;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  eg_fixed_base_destroy(c->gtab);
+  eg_fixed_base_destroy(c->Ktab);
+  for (auto& b : c->ws)
+    if (b.ptr) hipFree(b.ptr);
+  for (auto& kv : c->cache)
+    if (kv.second.ptr) hipFree(kv.second.ptr);
+  if (c->d) hipFree(c->d);
+  if (c->d_q) hipFree(c->d_q);
+  if (c->d_qbar) hipFree(c->d_qbar);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_sync(eg_ctx* c) {
+  if (!c) return fail(EG_ERR_ARG, "null ctx");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return EG_OK;
+}
+
+extern "C" eg_fixed_base* eg_ctx_g_table(eg_ctx* c) { return c ? c->gtab : nullptr; }
+
+extern "C" int eg_fixed_base_create(eg_ctx* c, const uint8_t base_be[512], int wbits, eg_fixed_base** out) {
+  if (!c || !base_be || !out) return fail(EG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  return fb_create_locked(c, base_be, wbits, out);
+}
+
+// ------------------------------------------------------------------------------
+// batched group ops (host buffers)
+// ------------------------------------------------------------------------------
+struct Locked {
+  std::lock_guard<std::mutex> lk;
+  explicit Locked(eg_ctx* c) : lk(c->mu) { hipSetDevice(c->device); }
+};
+
+static int upload(eg_ctx* c, Slot s, const void* h, size_t bytes, void** d) {
+  int rc = ws_get(c, s, bytes, d);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(*d, h, bytes, hipMemcpyHostToDevice, c->stream));
+  return EG_OK;
+}
+
+static int pow_host(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint32_t exp_bytes, bool exp_shared,
+                    uint8_t* out_be, size_t n, const FbTab* fbonly) {
+  uint8_t *d_base = nullptr, *d_exp = nullptr, *d_out = nullptr;
+  uint32_t *d_e = nullptr, *d_o = nullptr, *d_jobs = nullptr;
+  int rc;
+  const size_t nexp = exp_shared ? 1 : n;
+  if ((rc = upload(c, W_EXP, exp_be, nexp * exp_bytes, (void**)&d_exp))) return rc;
+  PowShape S{};
+  S.nout = 1;
+  S.exp_bytes = exp_bytes;
+  std::vector<uint32_t> jobs(n * kJobWords, kNone);
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t* J = &jobs[i * kJobWords];
+    J[0] = fbonly ? kNone : (uint32_t)i;
+    J[1] = exp_shared ? 0u : (uint32_t)i;
+    J[3] = (uint32_t)i;
+    J[5] = (uint32_t)i;
+  }
+  if (fbonly) {
+    S.has_base = 0;
+    S.nfb[0] = 1;
+    S.tab[0][0] = 0;
+  } else {
+    S.has_base = 1;
+    if ((rc = upload(c, W_IN0, base_be, n * 512, (void**)&d_base))) return rc;
+    if ((rc = ws_get(c, W_E0, n * kW * 4, (void**)&d_e))) return rc;
+    if ((rc = launch_import(c, d_base, n, d_e, nullptr))) return rc;
+  }
+  if ((rc = upload(c, W_JOBS, jobs.data(), jobs.size() * 4, (void**)&d_jobs))) return rc;
+  if ((rc = ws_get(c, W_E1, n * kW * 4, (void**)&d_o))) return rc;
+  FbTab f0 = fbonly ? *fbonly : c->gtab->tab();
+  if ((rc = launch_pow(c, S, d_jobs, n, d_e, d_exp, d_o, f0, f0))) return rc;
+  if ((rc = ws_get(c, W_OUT, n * 512, (void**)&d_out))) return rc;
+  if ((rc = launch_export(c, d_o, n, d_out))) return rc;
+  HIPCHK(hipMemcpyAsync(out_be, d_out, n * 512, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return EG_OK;
+}
+
+extern "C" int eg_powp_batch(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n) {
+  if (!c || (n && (!base_be || !exp_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!n) return EG_OK;
+  Locked L(c);
+  return pow_host(c, base_be, exp_be, 32, false, out_be, n, nullptr);
+}
+
+extern "C" int eg_fb_pow_batch(eg_fixed_base* fb, const uint8_t* exp_be, uint8_t* out_be, size_t n) {
+  if (!fb || (n && (!exp_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!n) return EG_OK;
+  eg_ctx* c = fb->ctx;
+  Locked L(c);
+  FbTab t = fb->tab();
+  return pow_host(c, nullptr, exp_be, 32, false, out_be, n, &t);
+}
+
+extern "C" int eg_multinv_batch(eg_ctx* c, const uint8_t* a_be, uint8_t* out_be, size_t n) {
+  if (!c || (n && (!a_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!n) return EG_OK;
+  Locked L(c);
+  // a^(p-2): p is odd and > 2, so subtracting 2 only touches the low word(s)
+  uint8_t e[512];
+  std::memcpy(e, c->p_be, 512);
+  int i = 511;
+  uint32_t borrow = 2;
+  while (borrow && i >= 0) {
+    const uint32_t v = e[i];
+    e[i] = (uint8_t)(v - borrow);
+    borrow = v < borrow ? 1 : 0;
+    --i;
+  }
+  return pow_host(c, a_be, e, 512, true, out_be, n, nullptr);
+}
+
+extern "C" int eg_multp_batch(eg_ctx* c, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be, size_t n) {
+  if (!c || (n && (!a_be || !b_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!n) return EG_OK;
+  Locked L(c);
+  uint8_t *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
+  uint32_t *ea = nullptr, *eb = nullptr;
+  int rc;
+  if ((rc = upload(c, W_IN0, a_be, n * 512, (void**)&d_a))) return rc;
+  if ((rc = upload(c, W_IN1, b_be, n * 512, (void**)&d_b))) return rc;
+  if ((rc = ws_get(c, W_E0, n * kW * 4, (void**)&ea))) return rc;
+  if ((rc = ws_get(c, W_E1, n * kW * 4, (void**)&eb))) return rc;
+  if ((rc = launch_import(c, d_a, n, ea, nullptr))) return rc;
+  if ((rc = launch_import(c, d_b, n, eb, nullptr))) return rc;
+  LAUNCH_F(c, k_mul, dim3(grid_for(n)), c->d, ea, 1u, eb, 1u, (uint32_t)n, ea, 1u);
+  HIPCHK(hipGetLastError());
+  if ((rc = ws_get(c, W_OUT, n * 512, (void**)&d_out))) return rc;
+  if ((rc = launch_export(c, ea, n, d_out))) return rc;
+  HIPCHK(hipMemcpyAsync(out_be, d_out, n * 512, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return EG_OK;
+}
+
+extern "C" int eg_prod_reduce(eg_ctx* c, const uint8_t* elems_be, size_t groups, size_t len, uint8_t* out_be) {
+  if (!c || (groups && (!elems_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!groups) return EG_OK;
+  Locked L(c);
+  if (len == 0) {
+    // empty product = 1
+    std::memset(out_be, 0, groups * 512);
+    for (size_t g = 0; g < groups; ++g) out_be[g * 512 + 511] = 1;
+    return EG_OK;
+  }
+  const size_t n = groups * len;
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  uint32_t *e = nullptr, *o = nullptr;
+  int rc;
+  if ((rc = upload(c, W_IN0, elems_be, n * 512, (void**)&d_in))) return rc;
+  if ((rc = ws_get(c, W_E0, n * kW * 4, (void**)&e))) return rc;
+  if ((rc = launch_import(c, d_in, n, e, nullptr))) return rc;
+  if ((rc = ws_get(c, W_E1, groups * kW * 4, (void**)&o))) return rc;
+  if ((rc = run_prod(c, e, GroupMap{1, 1, 0, 0, (uint32_t)len}, groups, len, 1, o))) return rc;
+  if ((rc = ws_get(c, W_OUT, groups * 512, (void**)&d_out))) return rc;
+  if ((rc = launch_export(c, o, groups, d_out))) return rc;
+  HIPCHK(hipMemcpyAsync(out_be, d_out, groups * 512, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_profile_begin(eg_ctx* c) {
+  if (!c) return fail(EG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (auto& r : c->prof) {
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  c->prof.clear();
+  c->timing = true;
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, int* launches) {
+  if (!c) return fail(EG_ERR_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  double t = 0, m = 0;
+  for (auto& r : c->prof) {
+    float x = 0;
+    HIPCHK(hipEventElapsedTime(&x, r.a, r.b));
+    t += x;
+    m += r.mm;
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  if (ms) *ms = t;
+  if (mm) *mm = m;
+  if (launches) *launches = (int)c->prof.size();
+  c->prof.clear();
+  c->timing = false;
+  return EG_OK;
+}
+
+#include "eg_capi_ballot.inc"

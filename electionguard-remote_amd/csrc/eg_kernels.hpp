@@ -1,0 +1,628 @@
+// eg_kernels.hpp — HIP kernels for the batched ElectionGuard group path on gfx950.
+//
+// All kernels run one element per group of kT lanes (eg_bignum.hpp) with 256-thread
+// workgroups and keep every Montgomery multiply WAVE-UNIFORM: per-launch shape
+// parameters are kernel arguments and tail groups recompute a clamped element
+// instead of branching out, so the DPP lane exchanges inside mont_mul never read
+// a disabled lane.
+#pragma once
+#include "eg_bignum.hpp"
+#include "eg_sha256.hpp"
+
+namespace eg {
+
+constexpr int kBlock = 256;
+constexpr int kGroupsPerBlock = kBlock / kT;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+struct FbTab {
+  const uint32_t* data;  // (nwin << wbits) device elements, entry (k, d) = base^(d * 2^(wbits*k))
+  uint32_t wbits;
+  uint32_t nwin;
+};
+
+// Per-thread constants of the modulus (loaded once per kernel).  F = p is
+// Montgomery-friendly (n0 == 1); every kernel is instantiated for both and the host
+// picks one per context, so only one Montgomery body is inlined per kernel.
+template <bool F>
+struct Mont {
+  uint32_t p[kL];
+  uint32_t n0, mask;
+  __device__ __forceinline__ void load(const MontConsts* __restrict__ C) {
+    const uint32_t* s = C->p + glane() * kLP;
+#pragma unroll
+    for (int j = 0; j < kL; ++j) p[j] = s[j];
+    n0 = C->n0;
+    mask = kMask;  // (an opaque VGPR mask lets DPP+AND fuse but costs ~80 VGPRs of RA quality)
+  }
+  __device__ __forceinline__ void mul(uint32_t (&x)[kL], const uint32_t* y) const {
+    mont_mul<F>(x, y, p, n0, mask);
+  }
+};
+
+__device__ __forceinline__ uint32_t* group_slot() {
+  __shared__ uint32_t s_slots[kGroupsPerBlock * kYStride];
+  return s_slots + (threadIdx.x / kT) * kYStride;
+}
+__device__ __forceinline__ uint32_t group_id() { return blockIdx.x * kGroupsPerBlock + threadIdx.x / kT; }
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// x <- x * x
+template <bool F>
+__device__ __forceinline__ void msqr(const Mont<F>& M, uint32_t (&x)[kL], uint32_t* slot) {
+  regs_to_lds(slot, x);
+  wave_sync();
+  M.mul(x, slot);
+  wave_sync();
+}
+// x <- x * E  (E a device element in global memory)
+template <bool F>
+__device__ __forceinline__ void mmul_g(const Mont<F>& M, uint32_t (&x)[kL], uint32_t* slot,
+                                       const uint32_t* __restrict__ E) {
+  elem_to_lds(slot, E);
+  wave_sync();
+  M.mul(x, slot);
+  wave_sync();
+}
+
+// ---------------------------------------------------------------------------------
+// Big-endian bytes <-> Montgomery form.
+// ---------------------------------------------------------------------------------
+
+// Stage one 512-byte big-endian element into the group slot as 128 LE words.
+__device__ __forceinline__ void stage_be(uint32_t* slot, const uint8_t* __restrict__ be) {
+  constexpr int kPer = 32 / kT;  // uint4 per lane
+  const uint4* src = reinterpret_cast<const uint4*>(be);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int idx = glane() * kPer + k;  // BE words 4idx..4idx+3
+    const uint4 v = src[idx];
+    slot[127 - 4 * idx] = __builtin_bswap32(v.x);
+    slot[126 - 4 * idx] = __builtin_bswap32(v.y);
+    slot[125 - 4 * idx] = __builtin_bswap32(v.z);
+    slot[124 - 4 * idx] = __builtin_bswap32(v.w);
+  }
+}
+
+// out[i] = be[i] * R mod p (Montgomery form); lt_p[i] = (be[i] < p) if lt_p != null
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_import(const MontConsts* __restrict__ C,
+                                                   const uint8_t* __restrict__ be, uint32_t n,
+                                                   uint32_t* __restrict__ out, uint8_t* __restrict__ lt_p) {
+  const uint32_t gid = group_id();
+  const uint32_t e = gid < n ? gid : n - 1;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  stage_be(slot, be + (size_t)e * 512);
+  wave_sync();
+  uint32_t x[kL];
+#pragma unroll
+  for (int j = 0; j < kL; ++j) x[j] = bits27(slot, 27 * (glane() * kL + j));
+  if (lt_p != nullptr && glane() == 0) {
+    // lexicographic compare from the most significant word
+    int cmp = 0;
+    for (int w = 127; w >= 0 && cmp == 0; --w) {
+      const uint32_t a = slot[w], b = C->pw[w];
+      cmp = a < b ? -1 : (a > b ? 1 : 0);
+    }
+    if (gid < n) lt_p[gid] = cmp < 0 ? 1 : 0;
+  }
+  wave_sync();
+  elem_to_lds(slot, C->r2);
+  wave_sync();
+  M.mul(x, slot);
+  if (gid < n) store_elem(out + (size_t)gid * kW, x);
+}
+
+// Fully normalise a value held in the group slot (limbs in device format, value <= p)
+// by group-lane 0; maps p -> 0.  Then write 512 big-endian bytes.
+__device__ __forceinline__ void slot_to_be(const MontConsts* __restrict__ C, uint32_t* slot,
+                                           uint8_t* __restrict__ dst, bool do_store) {
+  if (glane() == 0) {
+    uint32_t carry = 0;
+    bool eq = true;
+    for (int a = 0; a < kN; ++a) {
+      const int ia = (a / kL) * kLP + (a % kL);
+      const uint32_t v = slot[ia] + carry;
+      const uint32_t l = v & kMask;
+      carry = v >> kLimbBits;
+      slot[ia] = l;
+      eq &= (l == C->p[ia]);
+    }
+    if (eq) {
+      for (int a = 0; a < kW; ++a) slot[a] = 0;
+    }
+  }
+  wave_sync();
+  constexpr int kPer = 128 / kT;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int b = glane() * kPer + k;  // BE word index
+    const int w = 127 - b;             // LE word index
+    const int bit = 32 * w;
+    const int a = bit / kLimbBits, sh = bit - a * kLimbBits;
+    auto limb = [&](int i) -> uint64_t {
+      return i < kN ? (uint64_t)slot[(i / kL) * kLP + (i % kL)] : 0ull;
+    };
+    const uint64_t v = (limb(a) >> sh) | (limb(a + 1) << (kLimbBits - sh)) |
+                       (limb(a + 2) << (2 * kLimbBits - sh));
+    if (do_store) reinterpret_cast<uint32_t*>(dst)[b] = __builtin_bswap32((uint32_t)v);
+  }
+}
+
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_export(const MontConsts* __restrict__ C,
+                                                   const uint32_t* __restrict__ in, uint32_t n,
+                                                   uint8_t* __restrict__ be) {
+  const uint32_t gid = group_id();
+  const uint32_t e = gid < n ? gid : n - 1;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t x[kL];
+  load_elem(x, in + (size_t)e * kW);
+  elem_to_lds(slot, C->unit);
+  wave_sync();
+  M.mul(x, slot);  // leave the Montgomery domain: value in [0, p]
+  wave_sync();
+  regs_to_lds(slot, x);
+  wave_sync();
+  slot_to_be(C, slot, be + (size_t)gid * 512, gid < n);
+}
+
+// out[i*so] = a[i*sa] * b[i*sb]  (Montgomery form; strides in elements)
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_mul(const MontConsts* __restrict__ C,
+                                                const uint32_t* __restrict__ a, uint32_t sa,
+                                                const uint32_t* __restrict__ b, uint32_t sb, uint32_t n,
+                                                uint32_t* __restrict__ out, uint32_t so) {
+  const uint32_t gid = group_id();
+  const uint32_t e = gid < n ? gid : n - 1;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t x[kL];
+  load_elem(x, a + (size_t)e * sa * kW);
+  mmul_g(M, x, slot, b + (size_t)e * sb * kW);
+  if (gid < n) store_elem(out + (size_t)gid * so * kW, x);
+}
+
+// ---------------------------------------------------------------------------------
+// Exponentiation jobs.
+//   job record (kJobWords u32): base, e0, e1, out0, out1, f00, f01, f10, f11
+//   base    : element index of the variable base (kNone = no variable part)
+//   e0/e1   : scalar indices (32-B BE) of the variable-base exponents
+//   out0/1  : output element indices
+//   fXY     : scalar index of fixed-base term Y of output X
+// Launch-uniform shape: nout (1|2), nfb0/nfb1 (0..2), tab[X][Y] in {0,1} = which FbTab.
+// Variable part: fixed 4-bit window, table base^0..base^15 in per-group scratch.
+// ---------------------------------------------------------------------------------
+constexpr int kJobWords = 9;
+
+struct PowShape {
+  uint32_t has_base, nout, nfb[2], tab[2][2];
+  uint32_t exp_bytes;  // variable-base exponent length (32, or 512 for inverses)
+};
+
+__device__ __forceinline__ uint32_t be_digit(const uint8_t* __restrict__ e, int nbytes, int bit, int wb) {
+  uint32_t v = 0;
+  const int b0 = bit >> 3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = nbytes - 1 - (b0 + i);
+    if (idx >= 0) v |= (uint32_t)e[idx] << (8 * i);
+  }
+  return (v >> (bit & 7)) & ((1u << wb) - 1u);
+}
+
+template <bool F>
+__device__ __forceinline__ void fb_ladder(const Mont<F>& M, uint32_t (&x)[kL], uint32_t* slot, const FbTab& T,
+                                          const uint8_t* __restrict__ e, bool x_is_one) {
+  const uint32_t wb = T.wbits;
+  uint32_t k0 = 0;
+  if (x_is_one) {
+    const uint32_t d = be_digit(e, 32, 0, wb);
+    load_elem(x, T.data + (size_t)d * kW);
+    k0 = 1;
+  }
+#pragma unroll 1
+  for (uint32_t k = k0; k < T.nwin; ++k) {
+    const uint32_t d = be_digit(e, 32, k * wb, wb);
+    mmul_g(M, x, slot, T.data + ((size_t)(k << wb) + d) * kW);
+  }
+}
+
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_pow(const MontConsts* __restrict__ C, PowShape S,
+                                                const uint32_t* __restrict__ jobs, uint32_t njobs,
+                                                const uint32_t* __restrict__ elems,
+                                                const uint8_t* __restrict__ scalars,
+                                                uint32_t* __restrict__ out, uint32_t* __restrict__ scratch,
+                                                FbTab fb0, FbTab fb1) {
+  const uint32_t gid = group_id();
+  const uint32_t jb = gid < njobs ? gid : njobs - 1;
+  const uint32_t* J = jobs + (size_t)jb * kJobWords;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t x[kL];
+  uint32_t* tbl = scratch + (size_t)gid * 16 * kW;
+  if (S.has_base) {
+    const uint32_t* B = elems + (size_t)J[0] * kW;
+    // table: one, B, B^2 .. B^15
+    {
+      uint32_t one[kL];
+      load_elem(one, C->one);
+      store_elem(tbl, one);
+    }
+    load_elem(x, B);
+    store_elem(tbl + kW, x);
+    elem_to_lds(slot, B);
+    wave_sync();
+#pragma unroll 1
+    for (int k = 2; k < 16; ++k) {
+      M.mul(x, slot);
+      store_elem(tbl + (size_t)k * kW, x);
+    }
+    wave_sync();
+  }
+#pragma unroll 1
+  for (uint32_t o = 0; o < S.nout; ++o) {
+    bool x_is_one = true;
+    if (S.has_base) {
+      const uint8_t* e = scalars + (size_t)J[1 + o] * S.exp_bytes;
+      const int nwin = (int)S.exp_bytes * 2;
+      load_elem(x, tbl + (size_t)(e[0] >> 4) * kW);
+#pragma unroll 1
+      for (int w = 1; w < nwin; ++w) {
+        msqr(M, x, slot);
+        msqr(M, x, slot);
+        msqr(M, x, slot);
+        msqr(M, x, slot);
+        const uint32_t byte = e[w >> 1];
+        const uint32_t d = (w & 1) ? (byte & 15u) : (byte >> 4);
+        mmul_g(M, x, slot, tbl + (size_t)d * kW);
+      }
+      x_is_one = false;
+    }
+#pragma unroll 1
+    for (uint32_t t = 0; t < S.nfb[o]; ++t) {
+      const FbTab& T = S.tab[o][t] ? fb1 : fb0;
+      fb_ladder(M, x, slot, T, scalars + (size_t)J[5 + 2 * o + t] * 32, x_is_one);
+      x_is_one = false;
+    }
+    if (x_is_one) load_elem(x, C->one);
+    if (gid < njobs) store_elem(out + (size_t)J[3 + o] * kW, x);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Product reduction.  Group g is addressed by a mixed-radix decomposition
+//   g = (d2 * R1 + d1) * R0 + d0,  offset(g) = d2*M2 + d1*M1 + d0*M0   (elements)
+// and its k-th element sits at offset(g) + k*stride.  Job j -> group j / nchunk,
+// chunk j % nchunk; every job runs exactly `chunk`-1 multiplies (missing elements
+// are R mod p, the Montgomery one) so all groups of a wave stay in lock-step.
+// ---------------------------------------------------------------------------------
+struct GroupMap {
+  uint32_t R0, R1, M0, M1, M2;
+  __device__ __forceinline__ size_t offset(uint32_t g) const {
+    const uint32_t d0 = g % R0, t = g / R0;
+    const uint32_t d1 = t % R1, d2 = t / R1;
+    return (size_t)d2 * M2 + (size_t)d1 * M1 + (size_t)d0 * M0;
+  }
+};
+
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_prod(const MontConsts* __restrict__ C,
+                                                 const uint32_t* __restrict__ in, GroupMap gm, uint32_t ngroups,
+                                                 uint32_t len, uint32_t stride, uint32_t chunk,
+                                                 uint32_t nchunk, uint32_t* __restrict__ out) {
+  const uint32_t gid = group_id();
+  const uint32_t njobs = ngroups * nchunk;
+  const uint32_t jb = gid < njobs ? gid : njobs - 1;
+  const uint32_t g = jb / nchunk, c = jb % nchunk;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t x[kL];
+  const size_t base = gm.offset(g);
+  const uint32_t k0 = c * chunk;
+  load_elem(x, in + (base + (size_t)k0 * stride) * kW);
+#pragma unroll 1
+  for (uint32_t k = 1; k < chunk; ++k) {
+    const uint32_t kk = k0 + k;
+    const uint32_t* E = kk < len ? in + (base + (size_t)kk * stride) * kW : C->one;
+    mmul_g(M, x, slot, E);
+  }
+  if (gid < njobs) store_elem(out + (size_t)gid * kW, x);
+}
+
+// ---------------------------------------------------------------------------------
+// Fixed-base table construction.
+// k_sqr_chain: one group; P[j] = base^(2^j), j = 0..count-1 (Montgomery form).
+// k_fb_level : entries (k, 2^a + b) = (k, 2^a) * (k, b) for b in [1, 2^a).
+// ---------------------------------------------------------------------------------
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_sqr_chain(const MontConsts* __restrict__ C,
+                                                      const uint32_t* __restrict__ base, uint32_t count,
+                                                      uint32_t* __restrict__ P) {
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t x[kL];
+  load_elem(x, base);
+  const bool leader = group_id() == 0;
+  if (leader) store_elem(P, x);
+#pragma unroll 1
+  for (uint32_t j = 1; j < count; ++j) {
+    msqr(M, x, slot);
+    if (leader) store_elem(P + (size_t)j * kW, x);
+  }
+}
+
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_fb_level(const MontConsts* __restrict__ C, uint32_t* __restrict__ tab,
+                                                     uint32_t wbits, uint32_t nwin, uint32_t a) {
+  const uint32_t per = (1u << a) - 1u;
+  const uint32_t njobs = nwin * per;
+  const uint32_t gid = group_id();
+  const uint32_t jb = gid < njobs ? gid : njobs - 1;
+  const uint32_t k = jb / per, b = 1 + jb % per;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t x[kL];
+  uint32_t* row = tab + ((size_t)k << wbits) * kW;
+  load_elem(x, row + ((size_t)1 << a) * kW);
+  mmul_g(M, x, slot, row + (size_t)b * kW);
+  if (gid < njobs) store_elem(row + (size_t)((1u << a) + b) * kW, x);
+}
+
+// ---------------------------------------------------------------------------------
+// 256-bit scalar helpers (one thread per scalar).  Scalars are 32-B big-endian.
+// ---------------------------------------------------------------------------------
+struct U256 {
+  uint32_t w[8];  // little-endian words
+};
+__device__ __forceinline__ U256 ld256(const uint8_t* __restrict__ be) {
+  U256 r;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(be);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.w[i] = __builtin_bswap32(s[7 - i]);
+  return r;
+}
+__device__ __forceinline__ void st256(uint8_t* __restrict__ be, const U256& a) {
+  uint32_t* d = reinterpret_cast<uint32_t*>(be);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d[7 - i] = __builtin_bswap32(a.w[i]);
+}
+__device__ __forceinline__ bool lt256(const U256& a, const U256& b) {
+  for (int i = 7; i >= 0; --i) {
+    if (a.w[i] != b.w[i]) return a.w[i] < b.w[i];
+  }
+  return false;
+}
+__device__ __forceinline__ uint32_t add256(U256& a, const U256& b) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)a.w[i] + b.w[i];
+    a.w[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+__device__ __forceinline__ uint32_t sub256(U256& a, const U256& b) {
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (int64_t)a.w[i] - (int64_t)b.w[i];
+    a.w[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)(c & 1);
+}
+// (a + b) mod q for a, b < q
+__device__ __forceinline__ U256 addmod256(U256 a, const U256& b, const U256& q) {
+  const uint32_t carry = add256(a, b);
+  if (carry || !lt256(a, q)) sub256(a, q);
+  return a;
+}
+// (L * a) mod q for a < q, L < 2^32  (schoolbook + repeated subtraction-free fold)
+__device__ __forceinline__ U256 mulsmall_mod(const U256& a, uint32_t L, const U256& q) {
+  // r = L*a as 288-bit, then reduce by long division on the top word
+  uint32_t r[9];
+  uint64_t c = 0;
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)a.w[i] * L;
+    r[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  r[8] = (uint32_t)c;
+  U256 x;
+  for (int i = 0; i < 8; ++i) x.w[i] = r[i];
+  // subtract hi * q repeatedly: value = r8*2^256 + x; x < 2^256, r8 < L
+  // reduce via q's structure-free approach: while (r8 || x >= q) x -= q (with borrow into r8)
+  uint32_t hi = r[8];
+  while (hi != 0 || !lt256(x, q)) {
+    const uint32_t borrow = sub256(x, q);
+    hi -= borrow;
+  }
+  return x;
+}
+__device__ __forceinline__ U256 negmod(const U256& a, const U256& q) {
+  bool z = true;
+  for (int i = 0; i < 8; ++i) z &= (a.w[i] == 0);
+  if (z) return a;
+  U256 r = q;
+  sub256(r, a);
+  return r;
+}
+
+// (a - b) mod q for a, b < q
+__device__ __forceinline__ U256 submod256(U256 a, const U256& b, const U256& q) {
+  if (sub256(a, b)) add256(a, q);
+  return a;
+}
+// (a * b) mod q for a, b < q: left-to-right double-and-add (one thread; per proof, not per limb)
+__device__ __noinline__ U256 mulmod256(const U256& a, const U256& b, const U256& q) {
+  U256 r;
+  for (int k = 0; k < 8; ++k) r.w[k] = 0;
+  for (int bit = 255; bit >= 0; --bit) {
+    r = addmod256(r, r, q);
+    if ((a.w[bit >> 5] >> (bit & 31)) & 1u) r = addmod256(r, b, q);
+  }
+  return r;
+}
+
+// Encryption scalars, one thread per selection (nonces n = (R, u, c_fake, v_fake)):
+//   s_fake = v_fake + R*c_fake, s_gneg = m ? c_fake : -c_fake, mscal = m   (mod q)
+// (known-nonce simulation of the fake branch: a_f = g^s_fake, b_f = K^s_fake g^(+-c_fake))
+__global__ void k_enc_prep(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ votes,
+                           const uint8_t* __restrict__ nonces, uint32_t n, uint8_t* __restrict__ derived) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const U256 q = ld256(q_be);
+  const U256 R = ld256(nonces + ((size_t)i * 4 + 0) * 32);
+  const U256 cf = ld256(nonces + ((size_t)i * 4 + 2) * 32);
+  const U256 vf = ld256(nonces + ((size_t)i * 4 + 3) * 32);
+  const uint32_t m = votes[i] ? 1u : 0u;
+  const U256 sf = addmod256(vf, mulmod256(R, cf, q), q);
+  const U256 sg = m ? cf : negmod(cf, q);
+  U256 ms;
+  for (int k = 0; k < 8; ++k) ms.w[k] = 0;
+  ms.w[0] = m;
+  st256(derived + ((size_t)i * 3 + 0) * 32, ms);
+  st256(derived + ((size_t)i * 3 + 1) * 32, sf);
+  st256(derived + ((size_t)i * 3 + 2) * 32, sg);
+}
+
+// R_sum per contest (one thread per contest): sum of the spc selection nonces R
+__global__ void k_enc_rsum(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ nonces, uint32_t ncon,
+                           uint32_t spc, uint8_t* __restrict__ rsum) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ncon) return;
+  const U256 q = ld256(q_be);
+  U256 r;
+  for (int k = 0; k < 8; ++k) r.w[k] = 0;
+  for (uint32_t s = 0; s < spc; ++s) r = addmod256(r, ld256(nonces + (((size_t)j * spc + s) * 4) * 32), q);
+  st256(rsum + (size_t)j * 32, r);
+}
+
+// Finish the range proofs: c_real = c - c_fake, v_real = u - c_real*R; arrange by m.
+__global__ void k_enc_finish(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ votes,
+                             const uint8_t* __restrict__ nonces, const uint8_t* __restrict__ chal, uint32_t n,
+                             uint8_t* __restrict__ rproof) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const U256 q = ld256(q_be);
+  const U256 R = ld256(nonces + ((size_t)i * 4 + 0) * 32);
+  const U256 u = ld256(nonces + ((size_t)i * 4 + 1) * 32);
+  const U256 cf = ld256(nonces + ((size_t)i * 4 + 2) * 32);
+  const U256 vf = ld256(nonces + ((size_t)i * 4 + 3) * 32);
+  const U256 c = ld256(chal + (size_t)i * 32);
+  const U256 cr = submod256(c, cf, q);
+  const U256 vr = submod256(u, mulmod256(cr, R, q), q);
+  uint8_t* o = rproof + (size_t)i * 4 * 32;
+  if (votes[i]) {
+    st256(o + 0, cf); st256(o + 32, vf); st256(o + 64, cr); st256(o + 96, vr);
+  } else {
+    st256(o + 0, cr); st256(o + 32, vr); st256(o + 64, cf); st256(o + 96, vf);
+  }
+}
+
+// Generic response v = u - c*x mod q (x per item or shared when x_stride == 0);
+// writes proof (c, v) as 2 x 32 B.
+__global__ void k_response(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ u_be,
+                           const uint8_t* __restrict__ chal, const uint8_t* __restrict__ x_be, uint32_t x_stride,
+                           uint32_t n, uint8_t* __restrict__ proof) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const U256 q = ld256(q_be);
+  const U256 u = ld256(u_be + (size_t)i * 32);
+  const U256 c = ld256(chal + (size_t)i * 32);
+  const U256 x = ld256(x_be + (size_t)i * x_stride);
+  const U256 v = submod256(u, mulmod256(c, x, q), q);
+  st256(proof + (size_t)i * 64, c);
+  st256(proof + (size_t)i * 64 + 32, v);
+}
+
+// scalar derivation for the verifier (one thread per selection / contest)
+//   sel: out[i] = (q - c1_i) mod q  ; ok[i] = all of c0,v0,c1,v1 < q
+//   con: out[i] = (q - L*c_i mod q) ; ok[i] = c,v < q
+__global__ void k_scalar_prep(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ proofs,
+                              uint32_t n, uint32_t words_per, uint32_t neg_idx, uint32_t L,
+                              uint8_t* __restrict__ out, uint8_t* __restrict__ ok) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const U256 q = ld256(q_be);
+  bool good = true;
+  for (uint32_t k = 0; k < words_per; ++k) good &= lt256(ld256(proofs + ((size_t)i * words_per + k) * 32), q);
+  U256 c = ld256(proofs + ((size_t)i * words_per + neg_idx) * 32);
+  if (good) {
+    if (L != 1) c = mulsmall_mod(c, L, q);
+    c = negmod(c, q);
+  } else {
+    for (int k = 0; k < 8; ++k) c.w[k] = 0;
+  }
+  st256(out + (size_t)i * 32, c);
+  ok[i] = good ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------------
+// Fiat-Shamir hash + compare (one thread per proof).
+//   H = SHA256("|" + hex(e_0) + "|" + ... + "|") mod q, hex upper-case fixed width.
+//   selection: elements (qbar, alpha, beta, a0, b0, a1, b1), expect (c0 + c1) mod q
+//   contest  : elements (qbar, A, B, a, b),                   expect c
+// ---------------------------------------------------------------------------------
+struct HashSrc {
+  const uint8_t* ptr;  // base pointer
+  uint32_t bytes;      // element width (32 or 512)
+  uint32_t stride;     // bytes between consecutive proofs' elements
+};
+
+__global__ void __launch_bounds__(kBlock) k_hash_check(const uint8_t* __restrict__ q_be,
+                                                       const uint8_t* __restrict__ qbar_be, uint32_t n,
+                                                       uint32_t nsrc, HashSrc s0, HashSrc s1, HashSrc s2,
+                                                       HashSrc s3, HashSrc s4, HashSrc s5,
+                                                       const uint8_t* __restrict__ proofs,
+                                                       uint32_t proof_words, uint32_t cidx0, uint32_t cidx1,
+                                                       const uint8_t* __restrict__ pre_ok,
+                                                       const uint8_t* __restrict__ pre_ok2, uint32_t pre2_div,
+                                                       uint8_t* __restrict__ ok, uint8_t* __restrict__ out_h) {
+  __shared__ uint32_t s_buf[kBlock * 16];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Sha256 H;
+  H.init(s_buf + threadIdx.x * 16);
+  H.put('|');
+  H.put_hex(qbar_be, 32);
+  H.put('|');
+  const HashSrc src[6] = {s0, s1, s2, s3, s4, s5};
+  for (uint32_t k = 0; k < nsrc; ++k) {
+    H.put_hex(src[k].ptr + (size_t)i * src[k].stride, src[k].bytes);
+    H.put('|');
+  }
+  uint32_t dig[8];
+  H.finish(dig);
+  const U256 q = ld256(q_be);
+  U256 h;
+  for (int k = 0; k < 8; ++k) h.w[k] = dig[7 - k];
+  if (!lt256(h, q)) sub256(h, q);
+  if (out_h) st256(out_h + (size_t)i * 32, h);
+  if (!ok) return;
+  U256 c = ld256(proofs + ((size_t)i * proof_words + cidx0) * 32);
+  if (cidx1 != kNone) c = addmod256(c, ld256(proofs + ((size_t)i * proof_words + cidx1) * 32), q);
+  bool good = true;
+  for (int k = 0; k < 8; ++k) good &= (c.w[k] == h.w[k]);
+  if (pre_ok) good &= pre_ok[i] != 0;
+  if (pre_ok2) {
+    // pre_ok2 indexed per element pair: both pad/data of selection i must be < p
+    good &= pre_ok2[(size_t)i * pre2_div] != 0 && pre_ok2[(size_t)i * pre2_div + 1] != 0;
+  }
+  ok[i] = good ? 1 : 0;
+}
+
+}  // namespace eg

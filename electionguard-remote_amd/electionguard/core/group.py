@@ -1,0 +1,297 @@
+"""GroupContext / ElementModP / ElementModQ — host mirror of the upstream group layer.
+
+Reference boundary: the reference builds its one GroupContext in
+``KUtils.productionGroup()`` (src/main/java/electionguard/util/KUtils.java:10-12) and
+moves elements as fixed-width big-endian bytes (common.proto:6-16), importing them
+unchecked via ``new BigInteger(1, bytes)`` (ConvertCommonProto.java:41-57).
+
+Every mod-p operation here runs on the GPU through libeg_hip.so (batched C ABI);
+mod-q scalar arithmetic (256-bit, a few ops per proof) is host integer arithmetic.
+The per-element methods exist for API compatibility and are batches of one; the
+``*_batch`` methods are the intended drop-in entry points.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import native
+from .constants import G as _G, P as _P, Q as _Q, P_BYTES, Q_BYTES
+
+BytesLike = Union[bytes, bytearray, memoryview]
+
+
+def p_bytes(x: int) -> bytes:
+    return int(x).to_bytes(P_BYTES, "big")
+
+
+def q_bytes(x: int) -> bytes:
+    return int(x).to_bytes(Q_BYTES, "big")
+
+
+def as_p_array(elems: Union[np.ndarray, Sequence["ElementModP"], Sequence[int]]) -> np.ndarray:
+    """-> contiguous uint8 array of shape (n, 512)."""
+    if isinstance(elems, np.ndarray):
+        a = np.ascontiguousarray(elems, dtype=np.uint8)
+        return a.reshape(-1, P_BYTES)
+    out = np.empty((len(elems), P_BYTES), dtype=np.uint8)
+    for i, e in enumerate(elems):
+        out[i] = np.frombuffer(e.byteArray() if isinstance(e, ElementModP) else p_bytes(e), dtype=np.uint8)
+    return out
+
+
+def as_q_array(elems: Union[np.ndarray, Sequence["ElementModQ"], Sequence[int]]) -> np.ndarray:
+    if isinstance(elems, np.ndarray):
+        a = np.ascontiguousarray(elems, dtype=np.uint8)
+        return a.reshape(-1, Q_BYTES)
+    out = np.empty((len(elems), Q_BYTES), dtype=np.uint8)
+    for i, e in enumerate(elems):
+        out[i] = np.frombuffer(e.byteArray() if isinstance(e, ElementModQ) else q_bytes(e), dtype=np.uint8)
+    return out
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class GroupContext:
+    """GPU-backed GroupContext (one per device; calls are thread-safe)."""
+
+    def __init__(self, p: int, q: int, g: int, device: int = 0, fb_window_bits: int = 8):
+        self.p, self.q, self.g = p, q, g
+        self.r = (p - 1) // q if q and (p - 1) % q == 0 else None
+        self.device = device
+        self._lib = native.load()
+        self._p_be, self._q_be, self._g_be = p_bytes(p), q_bytes(q), p_bytes(g)
+        h = ctypes.c_void_p()
+        native.check(self._lib, "eg_ctx_create",
+                     self._lib.eg_ctx_create(native.buf(self._p_be), native.buf(self._q_be),
+                                             native.buf(self._g_be), device, ctypes.byref(h)))
+        self._ctx = h
+        self._lock = threading.Lock()
+        self._fb_window_bits = fb_window_bits
+        self.ONE_MOD_P = ElementModP(1, self)
+        self.ZERO_MOD_P = ElementModP(0, self)
+        self.G_MOD_P = ElementModP(g, self)
+        self.ZERO_MOD_Q = ElementModQ(0, self)
+        self.ONE_MOD_Q = ElementModQ(1, self)
+
+    # ---- lifetime ----
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.eg_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._ctx
+
+    # ---- element construction (ConvertCommonProto.importElementModP/Q semantics) ----
+    def binaryToElementModP(self, b: BytesLike) -> ElementModP:
+        return ElementModP(int.from_bytes(bytes(b), "big"), self)
+
+    def binaryToElementModQ(self, b: BytesLike) -> ElementModQ:
+        return ElementModQ(int.from_bytes(bytes(b), "big"), self)
+
+    def uIntToElementModQ(self, x: int) -> ElementModQ:
+        return ElementModQ(x % self.q, self)
+
+    # ---- batched group ops (the drop-in entry points) ----
+    def powP_batch(self, bases, exps) -> np.ndarray:
+        """out[i] = bases[i]^exps[i] mod p  (ElementModP.powP)."""
+        B, E = as_p_array(bases), as_q_array(exps)
+        if len(B) != len(E):
+            raise ValueError("bases/exps length mismatch")
+        out = np.empty_like(B)
+        if len(B):
+            native.check(self._lib, "eg_powp_batch",
+                         self._lib.eg_powp_batch(self._ctx, _ptr(B), _ptr(E), _ptr(out), len(B)))
+        return out
+
+    def gPowP_batch(self, exps) -> np.ndarray:
+        """out[i] = g^exps[i] mod p via the fixed-base table (GroupContext.gPowP)."""
+        E = as_q_array(exps)
+        out = np.empty((len(E), P_BYTES), dtype=np.uint8)
+        if len(E):
+            fb = self._lib.eg_ctx_g_table(self._ctx)
+            native.check(self._lib, "eg_fb_pow_batch",
+                         self._lib.eg_fb_pow_batch(fb, _ptr(E), _ptr(out), len(E)))
+        return out
+
+    def multP_batch(self, a, b) -> np.ndarray:
+        A, B = as_p_array(a), as_p_array(b)
+        if len(A) != len(B):
+            raise ValueError("length mismatch")
+        out = np.empty_like(A)
+        if len(A):
+            native.check(self._lib, "eg_multp_batch",
+                         self._lib.eg_multp_batch(self._ctx, _ptr(A), _ptr(B), _ptr(out), len(A)))
+        return out
+
+    def prodP_groups(self, elems, groups: int, length: int) -> np.ndarray:
+        """out[g] = prod_k elems[g*length + k] (Iterable<ElementModP>.multP())."""
+        A = as_p_array(elems)
+        if len(A) != groups * length:
+            raise ValueError("elems must hold groups*length elements")
+        out = np.empty((groups, P_BYTES), dtype=np.uint8)
+        if groups:
+            native.check(self._lib, "eg_prod_reduce",
+                         self._lib.eg_prod_reduce(self._ctx, _ptr(A), groups, length, _ptr(out)))
+        return out
+
+    def multInv_batch(self, a) -> np.ndarray:
+        A = as_p_array(a)
+        out = np.empty_like(A)
+        if len(A):
+            native.check(self._lib, "eg_multinv_batch",
+                         self._lib.eg_multinv_batch(self._ctx, _ptr(A), _ptr(out), len(A)))
+        return out
+
+    # ---- per-element convenience (batches of one) ----
+    def gPowP(self, e: Union["ElementModQ", int]) -> "ElementModP":
+        return ElementModP.from_bytes(self.gPowP_batch([e])[0], self)
+
+    def multP(self, *elems: "ElementModP") -> "ElementModP":
+        if not elems:
+            return self.ONE_MOD_P
+        return ElementModP.from_bytes(self.prodP_groups(list(elems), 1, len(elems))[0], self)
+
+    def dLogG(self, y: "ElementModP", max_result: int) -> Optional[int]:
+        """t with g^t = y, 0 <= t <= max_result (baby-step giant-step on the GPU)."""
+        from ..decrypt import dlog_g_batch
+
+        return dlog_g_batch(self, [y], max_result)[0]
+
+    def fixed_base(self, base: Union["ElementModP", int], window_bits: int = 8) -> "FixedBase":
+        return FixedBase(self, base, window_bits)
+
+    # ---- profiling of the dominant kernel ----
+    def profile_begin(self) -> None:
+        native.check(self._lib, "eg_ctx_profile_begin", self._lib.eg_ctx_profile_begin(self._ctx))
+
+    def profile_end(self):
+        ms, mm, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        native.check(self._lib, "eg_ctx_profile_end",
+                     self._lib.eg_ctx_profile_end(self._ctx, ctypes.byref(ms), ctypes.byref(mm), ctypes.byref(n)))
+        return ms.value, mm.value, n.value
+
+    def sync(self) -> None:
+        native.check(self._lib, "eg_ctx_sync", self._lib.eg_ctx_sync(self._ctx))
+
+
+class FixedBase:
+    """Accelerated base (``acceleratePow`` / PowRadix): radix table on the device."""
+
+    def __init__(self, group: GroupContext, base, window_bits: int = 8):
+        self.group = group
+        b = base.value if isinstance(base, ElementModP) else int(base)
+        self._be = p_bytes(b)
+        h = ctypes.c_void_p()
+        native.check(group._lib, "eg_fixed_base_create",
+                     group._lib.eg_fixed_base_create(group.handle, native.buf(self._be), window_bits,
+                                                     ctypes.byref(h)))
+        self._fb = h
+
+    def pow_batch(self, exps) -> np.ndarray:
+        E = as_q_array(exps)
+        out = np.empty((len(E), P_BYTES), dtype=np.uint8)
+        if len(E):
+            native.check(self.group._lib, "eg_fb_pow_batch",
+                         self.group._lib.eg_fb_pow_batch(self._fb, _ptr(E), _ptr(out), len(E)))
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "_fb", None):
+            self.group._lib.eg_fixed_base_destroy(self._fb)
+            self._fb = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass(frozen=True)
+class ElementModP:
+    """A member of Z_p (value unchecked on import, as upstream; ops reduce mod p)."""
+    value: int
+    group: GroupContext
+
+    @staticmethod
+    def from_bytes(b, group: GroupContext) -> "ElementModP":
+        return ElementModP(int.from_bytes(bytes(b), "big"), group)
+
+    def byteArray(self) -> bytes:
+        return p_bytes(self.value)
+
+    def powP(self, e: Union["ElementModQ", int]) -> "ElementModP":
+        return ElementModP.from_bytes(self.group.powP_batch([self], [e])[0], self.group)
+
+    def times(self, other: "ElementModP") -> "ElementModP":
+        return ElementModP.from_bytes(self.group.multP_batch([self], [other])[0], self.group)
+
+    def multInv(self) -> "ElementModP":
+        return ElementModP.from_bytes(self.group.multInv_batch([self])[0], self.group)
+
+    def div(self, other: "ElementModP") -> "ElementModP":
+        return self.times(other.multInv())
+
+    def inBounds(self) -> bool:
+        return 0 <= self.value < self.group.p
+
+    def __int__(self) -> int:
+        return self.value
+
+
+@dataclass(frozen=True)
+class ElementModQ:
+    """A member of Z_q; 256-bit scalar arithmetic on the host."""
+    value: int
+    group: GroupContext
+
+    def byteArray(self) -> bytes:
+        return q_bytes(self.value)
+
+    def _q(self) -> int:
+        return self.group.q
+
+    def __add__(self, o: "ElementModQ") -> "ElementModQ":
+        return ElementModQ((self.value + int(o)) % self._q(), self.group)
+
+    def __sub__(self, o: "ElementModQ") -> "ElementModQ":
+        return ElementModQ((self.value - int(o)) % self._q(), self.group)
+
+    def __mul__(self, o: "ElementModQ") -> "ElementModQ":
+        return ElementModQ((self.value * int(o)) % self._q(), self.group)
+
+    def __neg__(self) -> "ElementModQ":
+        return ElementModQ((-self.value) % self._q(), self.group)
+
+    def inBounds(self) -> bool:
+        return 0 <= self.value < self._q()
+
+    def __int__(self) -> int:
+        return self.value
+
+
+_PRODUCTION: dict = {}
+
+
+def productionGroup(device: int = 0) -> GroupContext:
+    """``KUtils.productionGroup()`` (KUtils.java:10-12): the EG 1.0 4096-bit group."""
+    g = _PRODUCTION.get(device)
+    if g is None:
+        g = GroupContext(_P, _Q, _G, device=device)
+        _PRODUCTION[device] = g
+    return g

@@ -1,0 +1,237 @@
+"""Trustee partial decryption and the mediator's combine — GPU-backed.
+
+Reference boundary: ``DecryptingTrusteeIF``, implemented remotely by
+``RemoteDecryptingTrusteeProxy`` (src/main/java/electionguard/decrypt/RemoteDecryptingTrusteeProxy.java:30,48-115)
+and served by ``RunRemoteDecryptingTrustee.directDecrypt`` / ``compensatedDecrypt``
+(RunRemoteDecryptingTrustee.java:180-208, 217-247).  Contract kept here:
+
+  * ``id()``, ``xCoordinate()``, ``electionPublicKey()``  (RemoteDecryptingTrusteeProxy.java:33-46)
+  * ``directDecrypt(group, texts, extendedBaseHash, nonce)`` -> list of
+    DirectDecryptionAndProof in text order (decrypting_trustee_rpc.proto:20-28)
+  * ``compensatedDecrypt(group, missingGuardianId, texts, extendedBaseHash, nonce)`` ->
+    list of CompensatedDecryptionAndProof (decrypting_trustee_rpc.proto:36-45)
+  * the whole text list is ONE batch (one GPU call), as the RPC is batched
+    (decrypting_trustee_rpc.proto:15-18).
+
+The mediator side restates ``Decryption.decrypt`` (RunRemoteDecryptor.java:261-262):
+verify each share's proof, Lagrange-combine compensated shares, M = prod M_i,
+T = B / M, t = dLog_g(T) (baby-step giant-step on the GPU).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import secrets
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .core import native
+from .core.group import GroupContext, as_p_array, p_bytes, q_bytes
+from .keyceremony import GuardianKeys, poly_eval
+
+
+@dataclass
+class GenericChaumPedersenProof:
+    c: int
+    v: int
+
+
+@dataclass
+class DirectDecryptionAndProof:
+    partialDecryption: int
+    proof: GenericChaumPedersenProof
+
+
+@dataclass
+class CompensatedDecryptionAndProof:
+    partialDecryption: int
+    proof: GenericChaumPedersenProof
+    recoveredPublicKeyShare: int
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _texts_array(texts) -> np.ndarray:
+    """texts: (n, 2, 512) uint8 array or a sequence of (pad, data) int pairs."""
+    if isinstance(texts, np.ndarray):
+        return np.ascontiguousarray(texts, dtype=np.uint8).reshape(-1, 2, 512)
+    out = np.empty((len(texts), 2, 512), dtype=np.uint8)
+    for i, (a, b) in enumerate(texts):
+        out[i, 0] = np.frombuffer(p_bytes(a), dtype=np.uint8)
+        out[i, 1] = np.frombuffer(p_bytes(b), dtype=np.uint8)
+    return out
+
+
+def _nonces(group: GroupContext, n: int, nonces) -> np.ndarray:
+    if nonces is None:
+        return np.stack([np.frombuffer(q_bytes(secrets.randbelow(group.q - 1) + 1), dtype=np.uint8)
+                         for _ in range(n)]) if n else np.empty((0, 32), np.uint8)
+    a = np.empty((n, 32), dtype=np.uint8)
+    for i, u in enumerate(nonces):
+        a[i] = np.frombuffer(q_bytes(int(u)), dtype=np.uint8)
+    return a
+
+
+def _be_int(row: np.ndarray) -> int:
+    return int.from_bytes(row.tobytes(), "big")
+
+
+def partial_decrypt_batch(group: GroupContext, secret: int, qbar: int, texts: np.ndarray,
+                          nonces: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """One GPU batch: M_i = pad_i^secret and proofs (c, v).  -> (M (n,512), proof (n,2,32))."""
+    n = texts.shape[0]
+    M = np.empty((n, 512), dtype=np.uint8)
+    pr = np.empty((n, 2, 32), dtype=np.uint8)
+    if n:
+        sb, qb = q_bytes(secret), q_bytes(qbar)
+        native.check(group._lib, "eg_trustee_decrypt_batch",
+                     group._lib.eg_trustee_decrypt_batch(group.handle, native.buf(sb), native.buf(qb), _ptr(texts),
+                                                         _ptr(nonces), n, _ptr(M), _ptr(pr)))
+    return M, pr
+
+
+class DecryptingTrustee:
+    """GPU-backed DecryptingTrusteeIF (one process per trustee, one GPU each)."""
+
+    def __init__(self, group: GroupContext, keys: GuardianKeys, commitments: Dict[str, List[int]]):
+        self.group = group
+        self.keys = keys
+        self.commitments = commitments  # every guardian's public commitments (for recovery keys)
+
+    def id(self) -> str:
+        return self.keys.gid
+
+    def xCoordinate(self) -> int:
+        return self.keys.x
+
+    def electionPublicKey(self) -> int:
+        return self.keys.public_key
+
+    def directDecrypt(self, group: GroupContext, texts, extendedBaseHash: int,
+                      nonce: Optional[Sequence[int]] = None) -> List[DirectDecryptionAndProof]:
+        T = _texts_array(texts)
+        M, pr = partial_decrypt_batch(group, self.keys.secret, extendedBaseHash, T, _nonces(group, len(T), nonce))
+        return [DirectDecryptionAndProof(_be_int(M[i]), GenericChaumPedersenProof(_be_int(pr[i, 0]), _be_int(pr[i, 1])))
+                for i in range(len(T))]
+
+    def recovery_public_key(self, missing_id: str) -> int:
+        """g^{P_l(x_i)} = prod_j K_{l,j}^{x_i^j} (GPU powP batch + product)."""
+        comm = self.commitments[missing_id]
+        q = self.group.q
+        exps = [pow(self.keys.x, j, q) for j in range(len(comm))]
+        pw = self.group.powP_batch(comm, exps)
+        return _be_int(self.group.prodP_groups(pw, 1, len(comm))[0])
+
+    def compensatedDecrypt(self, group: GroupContext, missingGuardianId: str, texts, extendedBaseHash: int,
+                           nonce: Optional[Sequence[int]] = None) -> List[CompensatedDecryptionAndProof]:
+        if missingGuardianId not in self.keys.shares_from:
+            raise KeyError(f"no share of {missingGuardianId}")
+        share = self.keys.shares_from[missingGuardianId]
+        T = _texts_array(texts)
+        M, pr = partial_decrypt_batch(group, share, extendedBaseHash, T, _nonces(group, len(T), nonce))
+        rk = self.recovery_public_key(missingGuardianId)
+        return [CompensatedDecryptionAndProof(_be_int(M[i]),
+                                              GenericChaumPedersenProof(_be_int(pr[i, 0]), _be_int(pr[i, 1])), rk)
+                for i in range(len(T))]
+
+
+def verify_shares(group: GroupContext, qbar: int, Ki: Sequence[int], texts, M: Sequence[int],
+                  proofs: Sequence[GenericChaumPedersenProof]) -> np.ndarray:
+    """a = g^v K_i^c, b = pad^v M^c; c == H(qbar, pad, data, a, b, M).  -> bool (n,)"""
+    T = _texts_array(texts)
+    n = len(T)
+    ok = np.zeros(n, dtype=np.uint8)
+    if n:
+        K = as_p_array(list(Ki))
+        Mm = as_p_array(list(M))
+        pr = np.empty((n, 2, 32), dtype=np.uint8)
+        for i, p in enumerate(proofs):
+            pr[i, 0] = np.frombuffer(q_bytes(p.c), dtype=np.uint8)
+            pr[i, 1] = np.frombuffer(q_bytes(p.v), dtype=np.uint8)
+        qb = q_bytes(qbar)
+        native.check(group._lib, "eg_verify_shares",
+                     group._lib.eg_verify_shares(group.handle, native.buf(qb), _ptr(K), _ptr(T), _ptr(Mm), _ptr(pr),
+                                                 n, _ptr(ok)))
+    return ok.astype(bool)
+
+
+def lagrange(xs: Sequence[int], xi: int, q: int) -> int:
+    num, den = 1, 1
+    for xj in xs:
+        if xj != xi:
+            num = num * xj % q
+            den = den * (xj - xi) % q
+    return num * pow(den, -1, q) % q
+
+
+def dlog_g_batch(group: GroupContext, ys, max_result: int) -> List[Optional[int]]:
+    """Baby-step giant-step on the GPU: t with g^t = y, 0 <= t <= max_result."""
+    Y = as_p_array(list(ys)) if not isinstance(ys, np.ndarray) else np.ascontiguousarray(ys).reshape(-1, 512)
+    n = len(Y)
+    if n == 0:
+        return []
+    m = math.isqrt(max_result) + 1
+    baby = group.gPowP_batch(list(range(m)))
+    table = {baby[j].tobytes(): j for j in range(m)}
+    q = group.q
+    giants = group.gPowP_batch([(q - (m * i) % q) % q for i in range(m + 1)])  # g^{-m i}
+    a = np.repeat(Y, m + 1, axis=0)
+    b = np.tile(giants, (n, 1))
+    prod = group.multP_batch(a, b).reshape(n, m + 1, 512)
+    out: List[Optional[int]] = []
+    for k in range(n):
+        res = None
+        for i in range(m + 1):
+            j = table.get(prod[k, i].tobytes())
+            if j is not None:
+                t = i * m + j
+                if t <= max_result:
+                    res = t
+                    break
+        out.append(res)
+    return out
+
+
+class Decryption:
+    """Mediator combine (``new Decryption(group, init, trustees, missing).decrypt(tally)``)."""
+
+    def __init__(self, group: GroupContext, qbar: int, trustees: Sequence, missing: Sequence[str],
+                 public_keys: Dict[str, int]):
+        self.group, self.qbar = group, qbar
+        self.trustees = list(trustees)
+        self.missing = list(missing)
+        self.public_keys = public_keys
+
+    def decrypt(self, tally: np.ndarray, max_count: int) -> List[Optional[int]]:
+        """tally: (n, 2, 512) encrypted per-selection totals -> plaintext counts."""
+        G = self.group
+        T = _texts_array(tally)
+        n = len(T)
+        xs = [t.xCoordinate() for t in self.trustees]
+        parts = []  # (n,512) arrays to multiply together
+        for tr in self.trustees:
+            res = tr.directDecrypt(G, T, self.qbar)
+            ok = verify_shares(G, self.qbar, [tr.electionPublicKey()] * n, T, [r.partialDecryption for r in res],
+                               [r.proof for r in res])
+            if not ok.all():
+                raise ValueError(f"invalid direct decryption proof from {tr.id()}")
+            parts.append(as_p_array([r.partialDecryption for r in res]))
+        for l in self.missing:
+            for tr in self.trustees:
+                res = tr.compensatedDecrypt(G, l, T, self.qbar)
+                ok = verify_shares(G, self.qbar, [r.recoveredPublicKeyShare for r in res], T,
+                                   [r.partialDecryption for r in res], [r.proof for r in res])
+                if not ok.all():
+                    raise ValueError(f"invalid compensated decryption proof from {tr.id()} for {l}")
+                w = lagrange(xs, tr.xCoordinate(), G.q)
+                Ml = as_p_array([r.partialDecryption for r in res])
+                parts.append(G.powP_batch(Ml, [w] * n))
+        k = len(parts)
+        stacked = np.ascontiguousarray(np.stack(parts, axis=1)).reshape(n * k, 512)
+        M = G.prodP_groups(stacked, n, k)
+        Tv = G.multP_batch(np.ascontiguousarray(T[:, 1]), G.multInv_batch(M))
+        return dlog_g_batch(G, Tv, max_count)

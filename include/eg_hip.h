@@ -1,0 +1,152 @@
+/* eg_hip.h — C ABI of the MI355X-native ElectionGuard group-operation library
+ * (libeg_hip.so).  Plain pointers and sizes only; no torch / HIP types.
+ *
+ * This is the drop-in boundary for the batched 4096-bit modexp path of
+ * JohnLCaron/electionguard-remote:
+ *
+ *   B1 — group layer.  The reference builds exactly one GroupContext, in
+ *        KUtils.productionGroup()  (src/main/java/electionguard/util/KUtils.java:10-12),
+ *        and moves elements across its wire boundary as fixed-width big-endian
+ *        bytes: ElementModP = 512 B (src/main/proto/common.proto:6-10),
+ *        ElementModQ = 32 B (common.proto:12-16), imported unchecked through
+ *        new BigInteger(1, bytes) (src/main/java/electionguard/util/ConvertCommonProto.java:41-57)
+ *        and exported with byteArray() (ConvertCommonProto.java:111-121).
+ *        Every buffer here uses that layout: element i of a batch occupies bytes
+ *        [512*i, 512*i+512) (or [32*i, 32*i+32) for exponents).
+ *   B2 — trustee plugin.  DecryptingTrusteeIF.directDecrypt / compensatedDecrypt,
+ *        implemented by RunRemoteDecryptingTrustee (:180-208, :217-247) and the
+ *        client proxy RemoteDecryptingTrusteeProxy (:48-115): see eg_trustee_*.
+ *
+ * Semantics shared by all entry points (match java.math.BigInteger):
+ *   - bases are reduced mod p (any 512-byte value is accepted, no subgroup check,
+ *     as ConvertCommonProto.importElementModP does not check);
+ *   - x^0 = 1 (including 0^0 = 1), 0^e = 0 for e > 0;
+ *   - exponents are used as given (not reduced mod q);
+ *   - outputs are canonical: 0 <= out < p, 512-byte big-endian.
+ * Status: 0 = EG_OK; non-zero on error with a thread-local message from
+ * eg_last_error().  No pointer is retained past a call except ctx / fixed-base
+ * handles.  Calls on one ctx are serialised on the ctx's HIP stream (thread-safe
+ * through an internal mutex); use one ctx per device.
+ * Host-pointer entry points copy over PCIe; the *_dev variants take device
+ * pointers (hipMalloc'd, e.g. torch CUDA tensors) and run asynchronously on the
+ * ctx stream (eg_ctx_sync to wait).
+ */
+#ifndef EG_HIP_H
+#define EG_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EG_OK 0
+#define EG_ERR_ARG 1
+#define EG_ERR_HIP 2
+#define EG_ERR_NOMEM 3
+#define EG_ERR_MODULUS 4
+#define EG_ERR_STATE 5
+
+#define EG_P_BYTES 512
+#define EG_Q_BYTES 32
+
+typedef struct eg_ctx eg_ctx;
+typedef struct eg_fixed_base eg_fixed_base;
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* eg_last_error(void);
+
+/* Library / device info: writes a NUL-terminated string (arch, limb layout). */
+int eg_version(char* buf, size_t len);
+
+/* GroupContext construction — replaces productionGroup(LOW_MEMORY_USE, Mode4096)
+ * (KUtils.java:10-12).  p must be odd, 2^4095 < p < 2^4096; q, g as in the group.
+ * device = HIP device ordinal (one ctx per device; trustee processes pin one GPU). */
+int eg_ctx_create(const uint8_t p_be[EG_P_BYTES], const uint8_t q_be[EG_Q_BYTES],
+                  const uint8_t g_be[EG_P_BYTES], int device, eg_ctx** out);
+int eg_ctx_destroy(eg_ctx* ctx);
+int eg_ctx_sync(eg_ctx* ctx);
+/* Kernel-level timing of the dominant kernel (k_pow, the windowed exponentiation):
+ * between begin and end every k_pow launch on the ctx stream is bracketed by HIP
+ * events; end synchronises and returns the summed device milliseconds, the
+ * algorithmic Montgomery multiplications those launches performed, and the
+ * number of launches. */
+int eg_ctx_profile_begin(eg_ctx* ctx);
+int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_muls, int* launches);
+/* Fixed-base table for g (built at ctx creation) — accessor. */
+eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
+
+/* Fixed-base radix table (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit
+ * windows).  window_bits in {4, 8, 11, 16}; table = ceil(256/w) * 2^w elements. */
+int eg_fixed_base_create(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], int window_bits,
+                         eg_fixed_base** out);
+int eg_fixed_base_destroy(eg_fixed_base* fb);
+
+/* ElementModP.powP(ElementModQ), variable base: out[i] = base[i]^exp[i] mod p. */
+int eg_powp_batch(eg_ctx* ctx, const uint8_t* base_be, const uint8_t* exp_be,
+                  uint8_t* out_be, size_t n);
+/* Fixed-base powP (gPowP / accelerated K.powP): out[i] = base^exp[i] mod p. */
+int eg_fb_pow_batch(eg_fixed_base* fb, const uint8_t* exp_be, uint8_t* out_be, size_t n);
+/* ElementModP.times: out[i] = a[i] * b[i] mod p. */
+int eg_multp_batch(eg_ctx* ctx, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be,
+                   size_t n);
+/* Iterable<ElementModP>.multP(): out[g] = prod_{k<len} elems[g*len + k] mod p
+ * (tally accumulation, runAccumulateBallots — RunRemoteWorkflowTest.java:151). */
+int eg_prod_reduce(eg_ctx* ctx, const uint8_t* elems_be, size_t groups, size_t len,
+                   uint8_t* out_be);
+/* ElementModP.multInv: out[i] = a[i]^-1 mod p (0 -> 0, as a^(p-2)). */
+int eg_multinv_batch(eg_ctx* ctx, const uint8_t* a_be, uint8_t* out_be, size_t n);
+
+/* ---- fused ballot verification + tally (Verifier(record, 11).verify() and
+ * runAccumulateBallots — RunRemoteWorkflowTest.java:151,179-182) ----
+ * Layout (all big-endian, ballot-major):
+ *   cts    : nballots * nsel * 2 * 512   (pad alpha, data beta) per selection
+ *   rproof : nballots * nsel * 4 * 32    (c0, v0, c1, v1)       per selection
+ *   cproof : nballots * ncontest * 2 * 32 (c, v)                per contest
+ * Selections are contest-major; contest k owns selections [k*spc, (k+1)*spc)
+ * (placeholders last: the tally skips the last `placeholders` of each contest).
+ * K_be = joint election key, qbar_be = extended base hash, limit = votesAllowed.
+ * Outputs: ok_sel[nballots*nsel], ok_contest[nballots*ncontest] (1 = valid),
+ * tally_be[ncontest*(spc-placeholders)*2*512] (may be NULL). */
+int eg_verify_ballots(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], const uint8_t qbar_be[EG_Q_BYTES],
+                      size_t nballots, size_t ncontest, size_t spc, size_t placeholders,
+                      uint32_t limit, const uint8_t* cts, const uint8_t* rproof,
+                      const uint8_t* cproof, uint8_t* ok_sel, uint8_t* ok_contest,
+                      uint8_t* tally_be);
+/* Same, device pointers, asynchronous on the ctx stream.  K must be registered
+ * first with eg_set_election_key (builds its fixed-base table once). */
+int eg_set_election_key(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], int window_bits);
+int eg_verify_ballots_dev(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nballots,
+                          size_t ncontest, size_t spc, size_t placeholders, uint32_t limit,
+                          const uint8_t* d_cts, const uint8_t* d_rproof, const uint8_t* d_cproof,
+                          uint8_t* d_ok_sel, uint8_t* d_ok_contest, uint8_t* d_tally_be);
+
+/* ---- batched encryption (batchEncryption, RunRemoteWorkflowTest.java:140-141) ----
+ * Per selection: plaintext m (0/1), nonces (R, u, c_fake, v_fake) as 4*32 B.
+ * Per contest: constant-proof nonce u (32 B).  Outputs cts / rproof / cproof in
+ * the eg_verify_ballots layout.  Requires eg_set_election_key. */
+int eg_encrypt_ballots(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nballots,
+                       size_t ncontest, size_t spc, const uint8_t* votes,
+                       const uint8_t* sel_nonces, const uint8_t* contest_nonces,
+                       uint8_t* cts, uint8_t* rproof, uint8_t* cproof);
+
+/* ---- trustee partial decryption (DecryptingTrusteeIF) ----
+ * directDecrypt (RunRemoteDecryptingTrustee.java:189-193): per text i,
+ *   M_i = pad_i^secret, proof (c, v) with a = g^u_i, b = pad_i^u_i,
+ *   c = H(qbar, pad_i, data_i, a, b, M_i), v = u_i - c*secret mod q.
+ * texts: n * 2 * 512 (pad, data); nonces: n * 32; out_M: n * 512; out_proof: n * 64 (c, v).
+ * compensatedDecrypt uses the same kernel with secret = P_l(x_i). */
+int eg_trustee_decrypt_batch(eg_ctx* ctx, const uint8_t secret_be[EG_Q_BYTES],
+                             const uint8_t qbar_be[EG_Q_BYTES], const uint8_t* texts,
+                             const uint8_t* nonces, size_t n, uint8_t* out_M, uint8_t* out_proof);
+/* Share-proof verification (mediator side of Decryption.decrypt,
+ * RunRemoteDecryptor.java:261-262): a = g^v K_i^c, b = pad^v M^c, check c. */
+int eg_verify_shares(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], const uint8_t* Ki_be,
+                     const uint8_t* texts, const uint8_t* M_be, const uint8_t* proof, size_t n,
+                     uint8_t* ok);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EG_HIP_H */

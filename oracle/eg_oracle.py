@@ -1,0 +1,419 @@
+"""CPU oracle for the batched 4096-bit modexp path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker.  The product path
+(``electionguard-remote_amd/``) never imports it.
+
+PARITY STATUS: parity unpinned.  The reference (JohnLCaron/electionguard-remote)
+holds no arithmetic: every group / ElGamal / proof / tally / decryption operation
+lives in the third-party module
+``electionguard-kotlin-multiplatform:electionguard-kotlin-multiplatform-jvm:1.0-SNAPSHOT``
+(build.gradle.kts:55), fetched from an authenticated Maven repo
+(build.gradle.kts:25-31) and absent here; there is no JDK either.  The
+reference's own tests pin nothing on this path
+(src/test/java/electionguard/keyceremony/RemoteKeyCeremonyTrusteeTest.java:10-14
+only asserts a protobuf builder is non-null).  What IS pinned:
+
+* group-level ops (powP, multP, multInv, products) are uniquely defined integers
+  mod p, so equality with ``java.math.BigInteger.modPow`` is a mathematical fact;
+  this module computes them with CPython ``int`` and is cross-checked against an
+  independent OpenSSL-BN restatement (``oracle/eg_oracle_c.c``);
+* the EG 1.0 group constants are re-derived from the spec construction and
+  self-checked (see :func:`derive_production_group`);
+* protocol-level restatements (ElGamal, Chaum-Pedersen, tally, threshold
+  decryption) follow the ElectionGuard 1.0 spec (cited by the reference at
+  src/main/proto/keyceremony_trustee_rpc.proto:40) and the reference's wire
+  formats (src/main/proto/common.proto:6-48, decrypting_trustee_rpc.proto:15-45).
+  The Fiat-Shamir hash pre-image format and nonce derivation are upstream and
+  unpinned; this oracle defines them (``hash_elems``) and the HIP path must match
+  this oracle bit-for-bit.
+
+Reference call sites into the restated upstream code:
+KUtils.java:11 (group), ConvertCommonProto.java:41-68 (element import, unchecked),
+RunRemoteWorkflowTest.java:140-141 (batchEncryption), :151 (runAccumulateBallots),
+:179-182 (Verifier), RunRemoteDecryptingTrustee.java:189-193 (directDecrypt),
+:227-232 (compensatedDecrypt), RunRemoteDecryptor.java:261-262 (Decryption.decrypt).
+"""
+from __future__ import annotations
+
+import hashlib
+import random
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+# --------------------------------------------------------------------------------------
+# Group constants (EG 1.0, ProductionMode.Mode4096 — KUtils.java:10-12)
+# --------------------------------------------------------------------------------------
+
+Q = 2**256 - 189
+# The low-order correction term of the EG 1.0 prime: p's middle 3584 bits are
+# floor(2^3584 * ln 2) + DELTA.  Pinned by q | p - 1 (2^-256 false-positive rate).
+DELTA = int(
+    "25f2da6646e943db028bd17d654a5fe9dc13e777f86b494195b2a55ba0d6d33e6d9d4f", 16)
+
+
+def derive_production_group() -> Tuple[int, int, int, int]:
+    """Re-derive (p, q, g, r) of the EG 1.0 4096-bit group from ln 2.
+
+    p = 2^4096 - 2^3840 + 2^256 * (floor(2^3584 ln2) + DELTA) + 2^256 - 1,
+    r = (p-1)/q, g = 2^r mod p.
+    """
+    import mpmath
+
+    with mpmath.workprec(3700):
+        x = int(mpmath.floor(mpmath.log(2) * mpmath.mpf(2) ** 3584))
+    p = 2**4096 - 2**3840 + 2**256 * (x + DELTA) + 2**256 - 1
+    assert (p - 1) % Q == 0, "q does not divide p-1: constants mis-derived"
+    r = (p - 1) // Q
+    g = pow(2, r, p)
+    assert g != 1 and pow(g, Q, p) == 1
+    return p, Q, g, r
+
+
+_GROUP_CACHE: Optional[Tuple[int, int, int, int]] = None
+
+
+def production_group() -> "Group":
+    global _GROUP_CACHE
+    if _GROUP_CACHE is None:
+        _GROUP_CACHE = derive_production_group()
+    p, q, g, r = _GROUP_CACHE
+    return Group(p, q, g)
+
+
+@dataclass(frozen=True)
+class Group:
+    p: int
+    q: int
+    g: int
+
+    # ---- group-level ops (upstream ElementModP / GroupContext) ----
+    def powP(self, b: int, e: int) -> int:
+        """ElementModP.powP: BigInteger.modPow semantics (base reduced mod p)."""
+        return pow(b % self.p, e, self.p)
+
+    def gPowP(self, e: int) -> int:
+        return pow(self.g, e, self.p)
+
+    def multP(self, a: int, b: int) -> int:
+        return (a * b) % self.p
+
+    def multInv(self, a: int) -> int:
+        return pow(a % self.p, -1, self.p)
+
+    def prodP(self, xs: Sequence[int]) -> int:
+        acc = 1
+        for x in xs:
+            acc = (acc * x) % self.p
+        return acc
+
+    def dlogG(self, y: int, max_result: int) -> Optional[int]:
+        """Discrete log base g by incremental table, as upstream dLogG (§8a a14)."""
+        acc = 1
+        for t in range(max_result + 1):
+            if acc == y:
+                return t
+            acc = (acc * self.g) % self.p
+        return None
+
+
+# --------------------------------------------------------------------------------------
+# Hashing (Fiat-Shamir).  Pre-image format: EG 1.0-style hash_elems with fixed-width
+# upper-case hex: "|" + "|".join(hex(e)) + "|", SHA-256, big-endian int mod q.
+# ElementModP -> 1024 hex chars (512 B BE, common.proto:6-10);
+# ElementModQ -> 64 hex chars (32 B BE, common.proto:12-16).  Unpinned upstream.
+# --------------------------------------------------------------------------------------
+
+def hexP(x: int) -> str:
+    return x.to_bytes(512, "big").hex().upper()
+
+
+def hexQ(x: int) -> str:
+    return x.to_bytes(32, "big").hex().upper()
+
+
+def hash_elems(q: int, *elems: Tuple[str, int]) -> int:
+    """elems: sequence of ("P"|"Q", value)."""
+    parts = [hexP(v) if kind == "P" else hexQ(v) for kind, v in elems]
+    msg = ("|" + "|".join(parts) + "|").encode("ascii")
+    return int.from_bytes(hashlib.sha256(msg).digest(), "big") % q
+
+
+# --------------------------------------------------------------------------------------
+# ElGamal + Chaum-Pedersen (compact (c, v) proofs: common.proto:23-28)
+# --------------------------------------------------------------------------------------
+
+@dataclass
+class Ciphertext:
+    pad: int   # alpha = g^R
+    data: int  # beta  = K^R g^m
+
+
+@dataclass
+class RangeProof:
+    """Disjunctive 0/1 Chaum-Pedersen proof, compact: (c0, v0), (c1, v1)."""
+    c0: int
+    v0: int
+    c1: int
+    v1: int
+
+
+@dataclass
+class GenericProof:
+    """GenericChaumPedersenProof(c, v) — common.proto:23-28."""
+    c: int
+    v: int
+
+
+def encrypt(G: Group, K: int, m: int, R: int) -> Ciphertext:
+    return Ciphertext(G.gPowP(R), G.multP(G.powP(K, R), G.gPowP(m)))
+
+
+def range_commitments(G: Group, K: int, ct: Ciphertext, pr: RangeProof) -> Tuple[int, int, int, int]:
+    """Verifier recompute: a_j = g^{v_j} alpha^{c_j}, b_j = K^{v_j} (beta g^-j)^{c_j}."""
+    p, q = G.p, G.q
+    a0 = G.multP(G.gPowP(pr.v0), G.powP(ct.pad, pr.c0))
+    b0 = G.multP(G.powP(K, pr.v0), G.powP(ct.data, pr.c0))
+    a1 = G.multP(G.gPowP(pr.v1), G.powP(ct.pad, pr.c1))
+    b1 = G.prodP([G.powP(K, pr.v1), G.powP(ct.data, pr.c1), G.gPowP((q - pr.c1) % q)])
+    return a0, b0, a1, b1
+
+
+def range_challenge(G: Group, qbar: int, ct: Ciphertext, a0: int, b0: int, a1: int, b1: int) -> int:
+    return hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data),
+                      ("P", a0), ("P", b0), ("P", a1), ("P", b1))
+
+
+def make_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, m: int, R: int,
+                     u: int, c_fake: int, v_fake: int) -> RangeProof:
+    """Prover with known nonce R and injected proof nonces (u, c_fake, v_fake)."""
+    q = G.q
+    f = 1 - m
+    a_real, b_real = G.gPowP(u), G.powP(K, u)
+    # fake branch f: a_f = g^{v_f} alpha^{c_f}, b_f = K^{v_f} (beta g^{-f})^{c_f}
+    a_fake = G.multP(G.gPowP(v_fake), G.powP(ct.pad, c_fake))
+    b_fake = G.prodP([G.powP(K, v_fake), G.powP(ct.data, c_fake), G.gPowP((q - f * c_fake) % q)])
+    if m == 0:
+        a0, b0, a1, b1 = a_real, b_real, a_fake, b_fake
+    else:
+        a0, b0, a1, b1 = a_fake, b_fake, a_real, b_real
+    c = range_challenge(G, qbar, ct, a0, b0, a1, b1)
+    c_real = (c - c_fake) % q
+    v_real = (u - c_real * R) % q
+    if m == 0:
+        return RangeProof(c_real, v_real, c_fake, v_fake)
+    return RangeProof(c_fake, v_fake, c_real, v_real)
+
+
+def verify_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, pr: RangeProof) -> bool:
+    q, p = G.q, G.p
+    if not (0 <= ct.pad < p and 0 <= ct.data < p):
+        return False
+    if not all(0 <= x < q for x in (pr.c0, pr.v0, pr.c1, pr.v1)):
+        return False
+    a0, b0, a1, b1 = range_commitments(G, K, ct, pr)
+    return (pr.c0 + pr.c1) % q == range_challenge(G, qbar, ct, a0, b0, a1, b1)
+
+
+def constant_commitments(G: Group, K: int, A: int, B: int, limit: int, pr: GenericProof) -> Tuple[int, int]:
+    q = G.q
+    a = G.multP(G.gPowP(pr.v), G.powP(A, pr.c))
+    b = G.prodP([G.powP(K, pr.v), G.powP(B, pr.c), G.gPowP((q - (limit * pr.c) % q) % q)])
+    return a, b
+
+
+def constant_challenge(G: Group, qbar: int, A: int, B: int, a: int, b: int) -> int:
+    return hash_elems(G.q, ("Q", qbar), ("P", A), ("P", B), ("P", a), ("P", b))
+
+
+def make_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, R_sum: int, u: int) -> GenericProof:
+    q = G.q
+    a, b = G.gPowP(u), G.powP(K, u)
+    c = constant_challenge(G, qbar, A, B, a, b)
+    return GenericProof(c, (u - c * R_sum) % q)
+
+
+def verify_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, limit: int, pr: GenericProof) -> bool:
+    if not (0 <= pr.c < G.q and 0 <= pr.v < G.q):
+        return False
+    a, b = constant_commitments(G, K, A, B, limit, pr)
+    return pr.c == constant_challenge(G, qbar, A, B, a, b)
+
+
+# --------------------------------------------------------------------------------------
+# Ballots (synthetic, seeded — restates RandomBallotProvider usage at
+# RunRemoteWorkflowTest.java:133-134; votesAllowed = 1, one placeholder per contest)
+# --------------------------------------------------------------------------------------
+
+@dataclass
+class Manifest:
+    n_contests: int = 4
+    n_selections: int = 5   # real selections per contest
+    votes_allowed: int = 1  # one placeholder selection per contest
+
+    @property
+    def sel_per_contest(self) -> int:
+        return self.n_selections + self.votes_allowed
+
+    @property
+    def sel_per_ballot(self) -> int:
+        return self.n_contests * self.sel_per_contest
+
+
+@dataclass
+class EncryptedBallot:
+    cts: List[Ciphertext]          # n_contests * sel_per_contest, placeholder last in each contest
+    proofs: List[RangeProof]
+    contest_proofs: List[GenericProof]
+
+
+def ballot_plaintexts(man: Manifest, rng: random.Random) -> List[int]:
+    votes = []
+    for _ in range(man.n_contests):
+        sel = [0] * man.sel_per_contest
+        sel[rng.randrange(man.n_selections)] = 1   # one-hot over real selections
+        votes.extend(sel)
+    return votes
+
+
+def encrypt_ballot(G: Group, K: int, qbar: int, man: Manifest, votes: List[int],
+                   rng: random.Random) -> EncryptedBallot:
+    q = G.q
+    cts, proofs, cproofs = [], [], []
+    spc = man.sel_per_contest
+    for c in range(man.n_contests):
+        R_sum = 0
+        for s in range(spc):
+            m = votes[c * spc + s]
+            R = rng.randrange(1, q)
+            u, cf, vf = rng.randrange(1, q), rng.randrange(q), rng.randrange(q)
+            ct = encrypt(G, K, m, R)
+            cts.append(ct)
+            proofs.append(make_range_proof(G, K, qbar, ct, m, R, u, cf, vf))
+            R_sum = (R_sum + R) % q
+        A = G.prodP([ct.pad for ct in cts[c * spc:(c + 1) * spc]])
+        B = G.prodP([ct.data for ct in cts[c * spc:(c + 1) * spc]])
+        cproofs.append(make_constant_proof(G, K, qbar, A, B, R_sum, rng.randrange(1, q)))
+    return EncryptedBallot(cts, proofs, cproofs)
+
+
+def verify_ballot(G: Group, K: int, qbar: int, man: Manifest, eb: EncryptedBallot) -> bool:
+    spc = man.sel_per_contest
+    ok = True
+    for c in range(man.n_contests):
+        for s in range(spc):
+            i = c * spc + s
+            ok &= verify_range_proof(G, K, qbar, eb.cts[i], eb.proofs[i])
+        A = G.prodP([ct.pad for ct in eb.cts[c * spc:(c + 1) * spc]])
+        B = G.prodP([ct.data for ct in eb.cts[c * spc:(c + 1) * spc]])
+        ok &= verify_constant_proof(G, K, qbar, A, B, man.votes_allowed, eb.contest_proofs[c])
+    return ok
+
+
+def accumulate_tally(G: Group, man: Manifest, ballots: Sequence[EncryptedBallot]) -> List[Ciphertext]:
+    """runAccumulateBallots (RunRemoteWorkflowTest.java:151): per real selection,
+    componentwise product of ciphertexts over cast ballots; placeholders excluded."""
+    spc = man.sel_per_contest
+    out = []
+    for c in range(man.n_contests):
+        for s in range(man.n_selections):
+            i = c * spc + s
+            out.append(Ciphertext(G.prodP([b.cts[i].pad for b in ballots]),
+                                  G.prodP([b.cts[i].data for b in ballots])))
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# Threshold decryption (DecryptingTrusteeIF — RunRemoteDecryptingTrustee.java:180-247;
+# Decryption.decrypt — RunRemoteDecryptor.java:261-262)
+# --------------------------------------------------------------------------------------
+
+@dataclass
+class Guardian:
+    gid: str
+    x: int                 # x-coordinate 1..n (RunRemoteKeyCeremony.java:268)
+    coeffs: List[int]      # polynomial a_{i,j}, a_{i,0} = s_i
+    commitments: List[int] # g^{a_{i,j}}
+
+    @property
+    def s(self) -> int:
+        return self.coeffs[0]
+
+    @property
+    def K(self) -> int:
+        return self.commitments[0]
+
+
+def poly_eval(coeffs: List[int], x: int, q: int) -> int:
+    acc = 0
+    for a in reversed(coeffs):
+        acc = (acc * x + a) % q
+    return acc
+
+
+def key_ceremony(G: Group, n: int, quorum: int, rng: random.Random) -> Tuple[List[Guardian], int]:
+    gs = []
+    for i in range(n):
+        co = [rng.randrange(1, G.q) for _ in range(quorum)]
+        gs.append(Guardian(f"guardian{i + 1}", i + 1, co, [G.gPowP(a) for a in co]))
+    K = G.prodP([g.K for g in gs])
+    return gs, K
+
+
+def direct_decrypt(G: Group, qbar: int, gd: Guardian, texts: Sequence[Ciphertext],
+                   nonces: Sequence[int]) -> List[Tuple[int, GenericProof]]:
+    """DirectDecryptionAndProof per text: M_i = A^{s_i} + generic CP proof
+    (decrypting_trustee_rpc.proto:25-28)."""
+    out = []
+    for ct, u in zip(texts, nonces):
+        M = G.powP(ct.pad, gd.s)
+        a, b = G.gPowP(u), G.powP(ct.pad, u)
+        c = hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data), ("P", a), ("P", b), ("P", M))
+        out.append((M, GenericProof(c, (u - c * gd.s) % G.q)))
+    return out
+
+
+def recovery_public_key(G: Group, missing: Guardian, x: int) -> int:
+    """g^{P_l(x)} = prod_j K_{l,j}^{x^j}."""
+    return G.prodP([G.powP(Kj, pow(x, j, G.q)) for j, Kj in enumerate(missing.commitments)])
+
+
+def compensated_decrypt(G: Group, qbar: int, gd: Guardian, missing: Guardian,
+                        texts: Sequence[Ciphertext], nonces: Sequence[int]) -> List[Tuple[int, GenericProof, int]]:
+    """CompensatedDecryptionAndProof (decrypting_trustee_rpc.proto:41-45)."""
+    share = poly_eval(missing.coeffs, gd.x, G.q)
+    rk = recovery_public_key(G, missing, gd.x)
+    out = []
+    for ct, u in zip(texts, nonces):
+        M = G.powP(ct.pad, share)
+        a, b = G.gPowP(u), G.powP(ct.pad, u)
+        c = hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data), ("P", a), ("P", b), ("P", M))
+        out.append((M, GenericProof(c, (u - c * share) % G.q), rk))
+    return out
+
+
+def verify_share(G: Group, qbar: int, Ki: int, ct: Ciphertext, M: int, pr: GenericProof) -> bool:
+    a = G.multP(G.gPowP(pr.v), G.powP(Ki, pr.c))
+    b = G.multP(G.powP(ct.pad, pr.v), G.powP(M, pr.c))
+    return pr.c == hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data), ("P", a), ("P", b), ("P", M))
+
+
+def lagrange(xs: Sequence[int], xi: int, q: int) -> int:
+    num, den = 1, 1
+    for xj in xs:
+        if xj != xi:
+            num = num * xj % q
+            den = den * (xj - xi) % q
+    return num * pow(den, -1, q) % q
+
+
+def combine(G: Group, ct: Ciphertext, direct: Dict[str, int], comp: Dict[str, Dict[str, int]],
+            avail_x: Dict[str, int], max_t: int) -> Optional[int]:
+    """M = prod direct M_i * prod_l prod_i M_{l,i}^{w_i}; T = B M^-1; t = dlog_g T."""
+    xs = list(avail_x.values())
+    M = G.prodP(list(direct.values()))
+    for _, shares in comp.items():
+        for gid, Mli in shares.items():
+            M = G.multP(M, G.powP(Mli, lagrange(xs, avail_x[gid], G.q)))
+    T = G.multP(ct.data, G.multInv(M))
+    return G.dlogG(T, max_t)

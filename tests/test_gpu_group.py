@@ -1,0 +1,104 @@
+"""Parity of the group-level ops (GroupContext / ElementModP, KUtils.java:10-12) on the
+GPU, through the C ABI, against the CPU oracle (CPython int == BigInteger semantics)."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import be2i
+
+pytestmark = pytest.mark.gpu
+
+
+def test_powp_random(group, oracle_group):
+    O = oracle_group
+    rng = random.Random(1)
+    n = 67  # ragged: not a multiple of the 32 elements of a workgroup
+    bases = [rng.randrange(2**4096) for _ in range(n)]  # includes values >= p (reduced, like BigInteger)
+    exps = [rng.randrange(2**256) for _ in range(n)]    # exponents used as given (not reduced mod q)
+    out = group.powP_batch(bases, exps)
+    for i in range(n):
+        assert be2i(out[i]) == O.powP(bases[i], exps[i]), i
+
+
+def test_powp_edges(group, oracle_group):
+    O = oracle_group
+    p, q = O.p, O.q
+    bases = [0, 0, 1, p - 1, p, p + 1, 2**4096 - 1, O.g, 2, p - 1]
+    exps = [0, 5, 2**256 - 1, 2, 7, 3, 2**256 - 1, q, q - 1, 0]
+    out = group.powP_batch(bases, exps)
+    for i in range(len(bases)):
+        assert be2i(out[i]) == O.powP(bases[i], exps[i]), (i, bases[i] % p, exps[i])
+
+
+def test_powp_empty(group):
+    assert group.powP_batch(np.empty((0, 512), np.uint8), np.empty((0, 32), np.uint8)).shape == (0, 512)
+
+
+def test_gpowp_fixed_base(group, oracle_group):
+    O = oracle_group
+    rng = random.Random(2)
+    exps = [0, 1, 2, O.q - 1, 2**256 - 1] + [rng.randrange(O.q) for _ in range(40)]
+    out = group.gPowP_batch(exps)
+    for i, e in enumerate(exps):
+        assert be2i(out[i]) == O.gPowP(e), i
+
+
+@pytest.mark.parametrize("wbits", [4, 11, 16])
+def test_fixed_base_windows(group, oracle_group, wbits):
+    O = oracle_group
+    rng = random.Random(wbits)
+    base = rng.randrange(O.p)
+    fb = group.fixed_base(base, window_bits=wbits)
+    exps = [0, 1, O.q - 1, 2**256 - 1] + [rng.randrange(O.q) for _ in range(20)]
+    out = fb.pow_batch(exps)
+    for i, e in enumerate(exps):
+        assert be2i(out[i]) == O.powP(base, e), i
+    fb.close()
+
+
+def test_multp(group, oracle_group):
+    O = oracle_group
+    rng = random.Random(3)
+    a = [rng.randrange(2**4096) for _ in range(50)] + [0, O.p, O.p - 1]
+    b = [rng.randrange(2**4096) for _ in range(50)] + [5, 3, O.p - 1]
+    out = group.multP_batch(a, b)
+    for i in range(len(a)):
+        assert be2i(out[i]) == O.multP(a[i], b[i]), i
+
+
+def test_prod_reduce(group, oracle_group):
+    O = oracle_group
+    rng = random.Random(4)
+    for groups, length in [(3, 1), (5, 7), (2, 100), (1, 33)]:
+        xs = [rng.randrange(O.p) for _ in range(groups * length)]
+        out = group.prodP_groups(xs, groups, length)
+        for g in range(groups):
+            assert be2i(out[g]) == O.prodP(xs[g * length:(g + 1) * length]), (groups, length, g)
+
+
+def test_multinv(group, oracle_group):
+    O = oracle_group
+    rng = random.Random(5)
+    xs = [1, O.p - 1, 2] + [rng.randrange(1, O.p) for _ in range(5)]
+    out = group.multInv_batch(xs)
+    for i, x in enumerate(xs):
+        assert be2i(out[i]) == O.multInv(x), i
+
+
+def test_generic_odd_modulus(oracle_group):
+    """A non-Montgomery-friendly odd 4096-bit modulus exercises the general CIOS path."""
+    from electionguard.core import GroupContext
+    rng = random.Random(6)
+    p = rng.randrange(2**4095, 2**4096) | 1
+    g = 3
+    G = GroupContext(p, oracle_group.q, g)
+    bases = [rng.randrange(2**4096) for _ in range(20)]
+    exps = [rng.randrange(2**256) for _ in range(20)]
+    out = G.powP_batch(bases, exps)
+    for i in range(20):
+        assert be2i(out[i]) == pow(bases[i] % p, exps[i], p), i
+    gout = G.gPowP_batch(exps)
+    for i in range(20):
+        assert be2i(gout[i]) == pow(g, exps[i], p), i
+    G.close()

@@ -1,0 +1,76 @@
+"""Parity of the trustee path (DecryptingTrusteeIF.directDecrypt / compensatedDecrypt,
+RunRemoteDecryptingTrustee.java:189-193,227-232) and the mediator combine
+(Decryption.decrypt, RunRemoteDecryptor.java:261-262) vs the oracle."""
+import random
+
+import numpy as np
+import pytest
+
+import eg_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_direct_and_compensated_shares_bitexact(group):
+    from electionguard.decrypt import partial_decrypt_batch
+    og = O.production_group()
+    rng = random.Random(21)
+    gs, K = O.key_ceremony(og, 3, 2, rng)
+    qbar = rng.randrange(og.q)
+    texts = [O.encrypt(og, K, rng.randrange(3), rng.randrange(1, og.q)) for _ in range(5)]
+    nonces = [rng.randrange(1, og.q) for _ in texts]
+    T = np.zeros((5, 2, 512), np.uint8)
+    for i, ct in enumerate(texts):
+        T[i, 0] = np.frombuffer(ct.pad.to_bytes(512, "big"), np.uint8)
+        T[i, 1] = np.frombuffer(ct.data.to_bytes(512, "big"), np.uint8)
+    N = np.stack([np.frombuffer(u.to_bytes(32, "big"), np.uint8) for u in nonces])
+    want = O.direct_decrypt(og, qbar, gs[0], texts, nonces)
+    M, pr = partial_decrypt_batch(group, gs[0].s, qbar, T, N)
+    for i, (Mi, p) in enumerate(want):
+        assert int.from_bytes(M[i].tobytes(), "big") == Mi
+        assert int.from_bytes(pr[i, 0].tobytes(), "big") == p.c
+        assert int.from_bytes(pr[i, 1].tobytes(), "big") == p.v
+    wantc = O.compensated_decrypt(og, qbar, gs[1], gs[2], texts, nonces)
+    share = O.poly_eval(gs[2].coeffs, gs[1].x, og.q)
+    M2, pr2 = partial_decrypt_batch(group, share, qbar, T, N)
+    for i, (Mi, p, rk) in enumerate(wantc):
+        assert int.from_bytes(M2[i].tobytes(), "big") == Mi
+        assert (int.from_bytes(pr2[i, 0].tobytes(), "big"), int.from_bytes(pr2[i, 1].tobytes(), "big")) == (p.c, p.v)
+
+
+def test_full_threshold_decryption(group):
+    """5 guardians, quorum 3, 2 missing (config C4 shape): tally counts recovered exactly."""
+    from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
+    from electionguard.decrypt import DecryptingTrustee, Decryption
+    from electionguard.keyceremony import key_ceremony
+    gk, K = key_ceremony(group, 5, 3, seed=3)
+    key = ElectionKey(group, K)
+    man = Manifest(2, 3, 1)
+    nr = np.random.default_rng(1)
+    nb = 9
+    votes = random_votes(nr, man, nb)
+    qbar = 12345
+    eb = batch_encryption(group, key, qbar, man, votes, random_scalars(nr, (nb, man.nsel, 4), group.q),
+                          random_scalars(nr, (nb, man.n_contests), group.q))
+    ok_s, ok_c, tally = Verifier(group, key, qbar, man).verify(eb)
+    assert ok_s.all() and ok_c.all()
+    comm = {g.gid: g.commitments for g in gk}
+    avail = [DecryptingTrustee(group, g, comm) for g in gk[:3]]
+    dec = Decryption(group, qbar, avail, [g.gid for g in gk[3:]], {g.gid: g.public_key for g in gk})
+    counts = dec.decrypt(tally, nb)
+    expected = votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].sum(axis=0).reshape(-1)
+    assert counts == [int(x) for x in expected]
+
+
+def test_verify_shares_rejects_bad_proof(group):
+    from electionguard.decrypt import GenericChaumPedersenProof, verify_shares
+    og = O.production_group()
+    rng = random.Random(22)
+    gs, K = O.key_ceremony(og, 2, 2, rng)
+    qbar = rng.randrange(og.q)
+    texts = [O.encrypt(og, K, 1, rng.randrange(1, og.q)) for _ in range(3)]
+    res = O.direct_decrypt(og, qbar, gs[0], texts, [rng.randrange(1, og.q) for _ in texts])
+    proofs = [GenericChaumPedersenProof(p.c, p.v) for _, p in res]
+    proofs[1] = GenericChaumPedersenProof(proofs[1].c, (proofs[1].v + 1) % og.q)
+    ok = verify_shares(group, qbar, [gs[0].K] * 3, [(t.pad, t.data) for t in texts], [m for m, _ in res], proofs)
+    assert list(ok) == [True, False, True]
