@@ -1,0 +1,230 @@
+"""Benchmark: ballots verified+tallied per second on the EG 1.0 4096-bit group.
+
+Workload (BASELINE.json configs[1]): per GPU, 10k synthetic ballots of 4 contests x 5
+selections (+1 placeholder each, 24 encrypted selections per ballot), batch-encrypted on
+the GPU in setup (untimed, reported separately), then ONE step = verify every ballot's
+disjunctive and contest proofs + homomorphic tally of all ballots, with the encrypted
+ballots already resident in HBM.  For N GPUs (torch.distributed.run, one rank per GPU)
+every rank verifies its own 10k-ballot shard (weak scaling) and the per-rank partial
+tallies are all-gathered over RCCL and folded mod p on rank 0.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the roofline definition.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "electionguard-remote_amd"))
+
+MAC_PER_MM = 2 * 128 * 128   # algorithmic u32xu32 MACs per 4096-bit Montgomery multiply
+PEAK_TMAC = 256 * 64 * 2.4e9 / 1e12   # 256 CUs x 64 v_mad_u64_u32 lanes/clk/CU x 2.4 GHz (profiles/r01_ubench_isa.txt)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--ballots", type=int, default=10000, help="ballots per GPU")
+    ap.add_argument("--contests", type=int, default=4)
+    ap.add_argument("--selections", type=int, default=5)
+    ap.add_argument("--fb-window", type=int, default=16, help="fixed-base radix window bits for g and K")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="ballots for the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption, random_scalars,
+                                      random_votes)
+    from electionguard.core import productionGroup
+    from electionguard.keyceremony import key_ceremony
+
+    group = productionGroup(local)
+    man = Manifest(a.contests, a.selections, 1)
+    nb = a.ballots
+    # synthetic election: 3 guardians, quorum 3 (configs[0] shape), same on every rank
+    gk, K = key_ceremony(group, 3, 3, seed=20241015)
+    key = ElectionKey(group, K, window_bits=a.fb_window)
+    qbar = int.from_bytes(b"electionguard-remote mi355x qbar".ljust(32, b"\0"), "big") % group.q
+    rng = np.random.default_rng(1000 + rank)
+    votes = random_votes(rng, man, nb)
+    sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
+    cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    eb = batch_encryption(group, key, qbar, man, votes, sn, cn)
+    enc_s = time.perf_counter() - t
+
+    dev = torch.device("cuda", local)
+    d_cts = torch.from_numpy(eb.cts).to(dev)
+    d_rp = torch.from_numpy(eb.rproof).to(dev)
+    d_cp = torch.from_numpy(eb.cproof).to(dev)
+    d_oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
+    d_okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
+    d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
+    gathered = torch.zeros((world, man.n_real, 2, 512), dtype=torch.uint8, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ver = Verifier(group, key, qbar, man)
+    final_tally = None
+
+    def step():
+        nonlocal final_tally
+        ver.verify_device(d_cts.data_ptr(), d_rp.data_ptr(), d_cp.data_ptr(), nb, d_oks.data_ptr(),
+                          d_okc.data_ptr(), d_tal.data_ptr())
+        group.sync()  # ctx stream -> torch stream ordering for the collective
+        ok = int(bool(d_oks.all().item() and d_okc.all().item()))
+        if world > 1:
+            flag.fill_(ok)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            dist.all_gather_into_tensor(gathered, d_tal)
+            if rank == 0:
+                parts = gathered.cpu().numpy()  # (world, n_real, 2, 512): fold mod p across ranks
+                g = np.ascontiguousarray(np.transpose(parts, (1, 2, 0, 3))).reshape(-1, 512)
+                final_tally = group.prodP_groups(g, man.n_real * 2, world).reshape(man.n_real, 2, 512)
+            ok = int(flag.item())
+        else:
+            final_tally = d_tal.cpu().numpy()
+        if not ok:
+            raise RuntimeError("verification failed on honest synthetic ballots")
+
+    for _ in range(a.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    group.profile_begin()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    group.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kms, kmm, klaunch = group.profile_end()
+    if dist:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    total_ballots = nb * world * a.steps
+    value = total_ballots / el
+    # algorithmic work of the dominant kernel (k_pow), from its own launch schedule
+    achieved = kmm * MAC_PER_MM / (kms / 1e3) / 1e12 if kms > 0 else None
+    mm_per_ballot = kmm / (nb * a.steps) if a.steps else None
+    out = {
+        "metric": "ballots verified+tallied/sec (node, 4096-bit group)",
+        "value": round(value, 2),
+        "unit": "ballots/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32xu32->u64 (radix-2^27 limbs)",
+        "data": "synthetic (seeded random one-hot ballots, GPU-encrypted with random nonces)",
+        "config": {
+            "workload": f"configs[1]: verify + homomorphic tally of {nb} ballots per GPU, "
+                        f"{a.contests} contests x {a.selections} selections (+1 placeholder), "
+                        "EG 1.0 4096-bit production group",
+            "ballots_per_gpu": nb,
+            "selections_per_ballot": man.nsel,
+            "fb_window_bits": a.fb_window,
+            "parallelism": f"ballot-sharded x{world}, RCCL all-gather of partial tallies",
+        },
+        "roofline": {
+            "bound": "valu-int",
+            "kernel": "k_pow (windowed Montgomery exponentiation + fused fixed-base terms)",
+            "achieved": round(achieved, 3) if achieved else None,
+            "peak": round(PEAK_TMAC, 2),
+            "unit": "TMAC/s (u32xu32+u64 v_mad_u64_u32)",
+            "frac": round(achieved / PEAK_TMAC, 4) if achieved else None,
+            "traffic": None,
+            "kernel_ms_per_launch": round(kms / max(klaunch, 1), 3),
+            "launches": klaunch,
+            "mont_mul_per_launch": round(kmm / max(klaunch, 1)),
+        },
+        "mont_mul_per_ballot": round(mm_per_ballot, 1) if mm_per_ballot else None,
+        "modexp_per_s_per_gpu": round((104 + 132) * value / world, 1),
+        "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
+    }
+    prof = ROOT / "profiles" / "r01_pmc_kpow.json"
+    if prof.exists():
+        try:
+            pm = json.loads(prof.read_text())
+            out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(a, man, eb, qbar, K, final_tally)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
+    """C restatement of the JVM path (OpenSSL BN Montgomery sliding window, 8-bit radix
+    fixed base = LOW_MEMORY_USE) on a bounded sample of the same ballots."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from eg_oracle_c import COracle
+    from electionguard.core import constants as C
+
+    threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    co = COracle(C.P, C.Q, C.G)
+    co.set_key(K)
+    s = min(a.cpu_sample, eb.n)
+    sub = eb.slice(0, s)
+    t = time.perf_counter()
+    ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, man.spc, 1, 1, sub.cts, sub.rproof, sub.cproof,
+                                      threads=threads)
+    dt = time.perf_counter() - t
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(s / dt, 3),
+        "unit": "ballots/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{s} of the same ballots (verify+tally, {man.nsel} selections each), {threads} threads "
+                  f"on {model or 'host CPU'}; OpenSSL BN_mod_exp_mont + 8-bit radix fixed base; "
+                  f"verdicts all valid: {bool(ok_s.all() and ok_c.all())}; wall {dt:.2f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()
