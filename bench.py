@@ -61,6 +61,7 @@ def main():
     from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption, random_scalars,
                                       random_votes)
     from electionguard.core import productionGroup
+    from electionguard.distributed import all_valid, gather_fold_tally
     from electionguard.keyceremony import key_ceremony
 
     group = productionGroup(local)
@@ -86,8 +87,6 @@ def main():
     d_oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
     d_okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
     d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-    gathered = torch.zeros((world, man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-    flag = torch.zeros(1, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     ver = Verifier(group, key, qbar, man)
     final_tally = None
@@ -97,18 +96,8 @@ def main():
         ver.verify_device(d_cts.data_ptr(), d_rp.data_ptr(), d_cp.data_ptr(), nb, d_oks.data_ptr(),
                           d_okc.data_ptr(), d_tal.data_ptr())
         group.sync()  # ctx stream -> torch stream ordering for the collective
-        ok = int(bool(d_oks.all().item() and d_okc.all().item()))
-        if world > 1:
-            flag.fill_(ok)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            dist.all_gather_into_tensor(gathered, d_tal)
-            if rank == 0:
-                parts = gathered.cpu().numpy()  # (world, n_real, 2, 512): fold mod p across ranks
-                g = np.ascontiguousarray(np.transpose(parts, (1, 2, 0, 3))).reshape(-1, 512)
-                final_tally = group.prodP_groups(g, man.n_real * 2, world).reshape(man.n_real, 2, 512)
-            ok = int(flag.item())
-        else:
-            final_tally = d_tal.cpu().numpy()
+        ok = all_valid(dist, bool(d_oks.all().item() and d_okc.all().item()), dev)
+        final_tally = gather_fold_tally(dist, d_tal, group.prodP_groups)
         if not ok:
             raise RuntimeError("verification failed on honest synthetic ballots")
 

@@ -1,0 +1,105 @@
+"""Generate the committed golden fixtures from the CPU oracle (oracle/eg_oracle.py).
+
+The reference (JohnLCaron/electionguard-remote) holds no fixtures or known-answer tests
+for this path and its arithmetic dependency cannot run here, so these
+vectors are produced by the oracle restatement and cross-checked against the
+independent OpenSSL-BN restatement (oracle/eg_oracle_c.c) by tests/test_oracle_golden.py.
+Run:  python tests/golden/make_golden.py   (deterministic; seeds below)
+"""
+import json
+import random
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent.parent / "oracle"))
+import eg_oracle as O  # noqa: E402
+
+
+def hx(x, n):
+    return int(x).to_bytes(n, "big").hex()
+
+
+def group_ops(G):
+    rng = random.Random(101)
+    p, q = G.p, G.q
+    bases = [0, 0, 1, p - 1, p, p + 1, 2**4096 - 1, G.g] + [rng.randrange(2**4096) for _ in range(40)]
+    exps = [0, 7, 2**256 - 1, 2, 3, q - 1, q, 1] + [rng.randrange(2**256) for _ in range(40)]
+    powp = [{"b": hx(b, 512), "e": hx(e, 32), "r": hx(G.powP(b, e), 512)} for b, e in zip(bases, exps)]
+    gexps = [0, 1, q - 1, 2**256 - 1] + [rng.randrange(q) for _ in range(28)]
+    gpow = [{"e": hx(e, 32), "r": hx(G.gPowP(e), 512)} for e in gexps]
+    mul = []
+    for _ in range(24):
+        a, b = rng.randrange(2**4096), rng.randrange(2**4096)
+        mul.append({"a": hx(a, 512), "b": hx(b, 512), "r": hx(G.multP(a, b), 512)})
+    inv = []
+    for x in [1, 2, p - 1] + [rng.randrange(1, p) for _ in range(5)]:
+        inv.append({"a": hx(x, 512), "r": hx(G.multInv(x), 512)})
+    prods = []
+    for length in (1, 5, 33):
+        xs = [rng.randrange(p) for _ in range(length)]
+        prods.append({"xs": [hx(x, 512) for x in xs], "r": hx(G.prodP(xs), 512)})
+    return {"powP": powp, "gPowP": gpow, "multP": mul, "multInv": inv, "prodP": prods}
+
+
+def ballots(G):
+    rng = random.Random(202)
+    gs, K = O.key_ceremony(G, 3, 2, rng)
+    qbar = rng.randrange(G.q)
+    man = O.Manifest(2, 3, 1)
+    out = {"K": hx(K, 512), "qbar": hx(qbar, 32), "manifest": [2, 3, 1], "ballots": []}
+    ebs = []
+    for b in range(3):
+        votes = O.ballot_plaintexts(man, rng)
+        state = rng.getstate()
+        eb = O.encrypt_ballot(G, K, qbar, man, votes, rng)
+        r2 = random.Random()
+        r2.setstate(state)
+        nonces, cnonces = [], []
+        for c in range(man.n_contests):
+            for s in range(man.sel_per_contest):
+                nonces.append([hx(r2.randrange(1, G.q), 32)] + [hx(r2.randrange(1, G.q), 32)] +
+                              [hx(r2.randrange(G.q), 32), hx(r2.randrange(G.q), 32)])
+            cnonces.append(hx(r2.randrange(1, G.q), 32))
+        ebs.append(eb)
+        out["ballots"].append({
+            "votes": votes, "nonces": nonces, "contest_nonces": cnonces,
+            "cts": [[hx(ct.pad, 512), hx(ct.data, 512)] for ct in eb.cts],
+            "rproofs": [[hx(v, 32) for v in (pr.c0, pr.v0, pr.c1, pr.v1)] for pr in eb.proofs],
+            "cproofs": [[hx(pr.c, 32), hx(pr.v, 32)] for pr in eb.contest_proofs],
+            "valid": O.verify_ballot(G, K, qbar, man, eb),
+        })
+    tally = O.accumulate_tally(G, man, ebs)
+    out["tally"] = [[hx(ct.pad, 512), hx(ct.data, 512)] for ct in tally]
+    return out
+
+
+def trustee(G):
+    rng = random.Random(303)
+    gs, K = O.key_ceremony(G, 3, 2, rng)
+    qbar = rng.randrange(G.q)
+    texts = [O.encrypt(G, K, rng.randrange(4), rng.randrange(1, G.q)) for _ in range(4)]
+    nonces = [rng.randrange(1, G.q) for _ in texts]
+    d = O.direct_decrypt(G, qbar, gs[0], texts, nonces)
+    c = O.compensated_decrypt(G, qbar, gs[1], gs[2], texts, nonces)
+    return {
+        "qbar": hx(qbar, 32),
+        "guardians": [{"x": g.x, "coeffs": [hx(a, 32) for a in g.coeffs],
+                       "commitments": [hx(k, 512) for k in g.commitments]} for g in gs],
+        "texts": [[hx(t.pad, 512), hx(t.data, 512)] for t in texts],
+        "nonces": [hx(u, 32) for u in nonces],
+        "direct": [{"M": hx(M, 512), "c": hx(p.c, 32), "v": hx(p.v, 32)} for M, p in d],
+        "compensated_by_x2_for_x3": [{"M": hx(M, 512), "c": hx(p.c, 32), "v": hx(p.v, 32),
+                                       "recovery": hx(rk, 512)} for M, p, rk in c],
+    }
+
+
+if __name__ == "__main__":
+    G = O.production_group()
+    (HERE / "group_ops.json").write_text(json.dumps(group_ops(G), indent=0))
+    (HERE / "ballots.json").write_text(json.dumps(ballots(G), indent=0))
+    (HERE / "trustee.json").write_text(json.dumps(trustee(G), indent=0))
+    p, q, g, r = O.derive_production_group()
+    (HERE / "constants.json").write_text(json.dumps({"p": hx(p, 512), "q": hx(q, 32), "g": hx(g, 512),
+                                                     "r": hx(r, 512)}, indent=0))
+    print("written")

@@ -1,0 +1,79 @@
+"""CPU: the N>1 path with world_size 2 over gloo — ballot shards, verdict all-reduce and
+the all-gather + mod-p fold of partial tallies (the fold is the oracle's product here;
+on the GPU it is GroupContext.prodP_groups)."""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import eg_oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fold_oracle(elems, groups, length):
+    G = O.production_group()
+    out = np.zeros((groups, 512), np.uint8)
+    for g in range(groups):
+        xs = [int.from_bytes(elems[g * length + k].tobytes(), "big") for k in range(length)]
+        out[g] = np.frombuffer(G.prodP(xs).to_bytes(512, "big"), np.uint8)
+    return out
+
+
+def _worker(rank, world, port, data, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from electionguard.distributed import all_valid, gather_fold_tally, shard_range
+    cts, n_real = data
+    a, b = shard_range(cts.shape[0], world, rank)
+    G = O.production_group()
+    # partial tally of this shard (oracle product stands in for the GPU reduction)
+    part = np.zeros((n_real, 2, 512), np.uint8)
+    for s in range(n_real):
+        for c in range(2):
+            part[s, c] = np.frombuffer(G.prodP([int.from_bytes(cts[i, s, c].tobytes(), "big")
+                                               for i in range(a, b)]).to_bytes(512, "big"), np.uint8)
+    ok = all_valid(dist, rank != 1 or True, torch.device("cpu"))
+    bad = all_valid(dist, rank == 0, torch.device("cpu"))
+    tally = gather_fold_tally(dist, torch.from_numpy(part), _fold_oracle)
+    if rank == 0:
+        q.put((ok, bad, tally.tobytes()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_tally_fold_equals_global_tally():
+    G = O.production_group()
+    rng = random.Random(5)
+    nb, n_real = 7, 3  # ragged shards 4 + 3
+    cts = np.zeros((nb, n_real, 2, 512), np.uint8)
+    for i in range(nb):
+        for s in range(n_real):
+            for c in range(2):
+                cts[i, s, c] = np.frombuffer(rng.randrange(1, G.p).to_bytes(512, "big"), np.uint8)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, (cts, n_real), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok, bad, tally = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok is True and bad is False
+    t = np.frombuffer(tally, np.uint8).reshape(n_real, 2, 512)
+    for s in range(n_real):
+        for c in range(2):
+            want = G.prodP([int.from_bytes(cts[i, s, c].tobytes(), "big") for i in range(nb)])
+            assert int.from_bytes(t[s, c].tobytes(), "big") == want

@@ -1,0 +1,68 @@
+"""CPU: host-side logic of the path (scalar generation, ballot layout, Lagrange, sharding)."""
+import random
+
+import numpy as np
+
+import eg_oracle as O
+
+
+def test_random_scalars_below_q():
+    from electionguard.ballot import random_scalars
+    rng = np.random.default_rng(3)
+    q = O.Q
+    s = random_scalars(rng, (1000, 4), q)
+    assert s.shape == (1000, 4, 32)
+    assert all(int.from_bytes(x.tobytes(), "big") < q for x in s.reshape(-1, 32))
+    tiny_q = 2**255 + 12345  # forces rejections
+    s2 = random_scalars(rng, (500,), tiny_q)
+    assert all(int.from_bytes(x.tobytes(), "big") < tiny_q for x in s2)
+
+
+def test_random_votes_one_hot_and_placeholders_zero():
+    from electionguard.ballot import Manifest, random_votes
+    man = Manifest(4, 5, 1)
+    v = random_votes(np.random.default_rng(1), man, 200).reshape(200, 4, 6)
+    assert (v.sum(axis=2) == 1).all() and (v[:, :, 5] == 0).all()
+
+
+def test_manifest_shape():
+    from electionguard.ballot import Manifest
+    m = Manifest(4, 5, 1)
+    assert (m.spc, m.nsel, m.n_real) == (6, 24, 20)
+
+
+def test_lagrange_matches_oracle_and_interpolates():
+    from electionguard.decrypt import lagrange
+    q = O.Q
+    rng = random.Random(4)
+    coeffs = [rng.randrange(q) for _ in range(3)]
+    xs = [1, 3, 5]
+    ys = [O.poly_eval(coeffs, x, q) for x in xs]
+    assert sum(lagrange(xs, x, q) * y for x, y in zip(xs, ys)) % q == coeffs[0]
+    assert all(lagrange(xs, x, q) == O.lagrange(xs, x, q) for x in xs)
+
+
+def test_shard_range_covers_exactly():
+    from electionguard.distributed import shard_range
+    for n in (0, 1, 7, 10000, 1000003):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_tally_group_layout_matches_oracle_order():
+    """accumulate_tally's (contest, selection, component) x ballots grouping."""
+    from electionguard.ballot import Manifest
+    man = Manifest(2, 3, 1)
+    nb = 4
+    cts = np.arange(nb * man.nsel * 2, dtype=np.int64).reshape(nb, man.nsel, 2)
+    sel = cts.reshape(nb, man.n_contests, man.spc, 2)[:, :, : man.n_selections]
+    g = np.transpose(sel, (1, 2, 3, 0)).reshape(-1, nb)
+    # group (k, s, c) must hold element (b, k*spc+s, c) for every ballot b
+    for k in range(2):
+        for s in range(3):
+            for c in range(2):
+                row = g[(k * 3 + s) * 2 + c]
+                assert list(row) == [cts[b, k * man.spc + s, c] for b in range(nb)]
