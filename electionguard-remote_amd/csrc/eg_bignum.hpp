@@ -58,14 +58,26 @@ __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u,
 __device__ __forceinline__ int glane() { return lane_id() & (kT - 1); }   // lane within element group
 __device__ __forceinline__ int gslot() { return lane_id() / kT; }        // group index within wave
 
+#ifndef EG_BCAST
+#define EG_BCAST 0  // 0: DPP (VALU), 1: ds_swizzle (LDS pipe, no VALU issue slot)
+#endif
+#ifndef EG_PLDS
+#define EG_PLDS 0   // 1: modulus limbs read from LDS instead of VGPRs
+#endif
+
 // Broadcast group-lane 0's value to the whole group.
 __device__ __forceinline__ uint32_t bcast_g0(uint32_t v) {
+#if EG_BCAST == 1
+  // bit-mode swizzle within 32 lanes: lane' = lane & and_mask (clears the in-group bits)
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, kT == 8 ? 0x0018 : 0x001C);
+#else
   uint32_t a = __builtin_amdgcn_mov_dpp(v, 0x00 /*quad_perm [0,0,0,0]*/, 0xF, 0xF, false);
   if constexpr (kT == 8) {
     // lanes 4-7 / 12-15 of every row take the value 4 lanes below (the group's lane 0)
     a = __builtin_amdgcn_update_dpp(a, a, 0x114 /*row_shr:4*/, 0xF, 0xA, false);
   }
   return a;
+#endif
 }
 
 // value from lane+1 within the DPP row (0 at the row end)
@@ -82,9 +94,9 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t v) {
 //   y : the group's LDS slot (kW words, device element format), value < 2p
 //   p : this lane's L modulus limbs
 // CIOS, one radix-2^27 digit of y per step; 2L v_mad_u64_u32 + ~5 VALU per step.
-template <bool FRIENDLY>
+template <bool FRIENDLY, class PT>
 __device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
-                                         const uint32_t (&p)[kL], uint32_t n0, uint32_t mask) {
+                                         const PT& p, uint32_t n0, uint32_t mask) {
   uint64_t acc[kL];
 #pragma unroll
   for (int j = 0; j < kL; ++j) acc[j] = 0;
@@ -137,13 +149,6 @@ __device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __re
       x[j] = ((uint32_t)d[j] & mask) + c;
     }
   }
-}
-
-// Generic dispatch on the friendliness of p (wave-uniform).
-__device__ __forceinline__ void mmul(uint32_t (&x)[kL], const uint32_t* y, const uint32_t (&p)[kL],
-                                     uint32_t n0, uint32_t mask, bool friendly) {
-  if (friendly) mont_mul<true>(x, y, p, n0, mask);
-  else mont_mul<false>(x, y, p, n0, mask);
 }
 
 // ---- element I/O between VGPRs, LDS slots and the device element format ----

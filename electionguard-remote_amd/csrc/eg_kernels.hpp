@@ -12,6 +12,9 @@
 namespace eg {
 
 constexpr int kBlock = 256;
+#ifndef EG_MIN_WAVES
+#define EG_MIN_WAVES 1  // __launch_bounds__ min waves per SIMD for the Montgomery kernels
+#endif
 constexpr int kGroupsPerBlock = kBlock / kT;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -26,12 +29,24 @@ struct FbTab {
 // picks one per context, so only one Montgomery body is inlined per kernel.
 template <bool F>
 struct Mont {
+#if EG_PLDS
+  const uint32_t* p;  // this lane's modulus block in LDS
+#else
   uint32_t p[kL];
+#endif
   uint32_t n0, mask;
+  // Must be called by every thread of the block (EG_PLDS stages p with a barrier).
   __device__ __forceinline__ void load(const MontConsts* __restrict__ C) {
+#if EG_PLDS
+    __shared__ uint32_t s_p[kW];
+    for (int i = threadIdx.x; i < kW; i += blockDim.x) s_p[i] = C->p[i];
+    __syncthreads();
+    p = s_p + glane() * kLP;
+#else
     const uint32_t* s = C->p + glane() * kLP;
 #pragma unroll
     for (int j = 0; j < kL; ++j) p[j] = s[j];
+#endif
     n0 = C->n0;
     mask = kMask;  // (an opaque VGPR mask lets DPP+AND fuse but costs ~80 VGPRs of RA quality)
   }
@@ -235,7 +250,7 @@ __device__ __forceinline__ void fb_ladder(const Mont<F>& M, uint32_t (&x)[kL], u
 }
 
 template <bool F>
-__global__ void __launch_bounds__(kBlock) k_pow(const MontConsts* __restrict__ C, PowShape S,
+__global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowShape S,
                                                 const uint32_t* __restrict__ jobs, uint32_t njobs,
                                                 const uint32_t* __restrict__ elems,
                                                 const uint8_t* __restrict__ scalars,
@@ -249,52 +264,83 @@ __global__ void __launch_bounds__(kBlock) k_pow(const MontConsts* __restrict__ C
   M.load(C);
   uint32_t x[kL];
   uint32_t* tbl = scratch + (size_t)gid * 16 * kW;
+  const uint32_t* B = S.has_base ? elems + (size_t)J[0] * kW : nullptr;
+  const int nwin = (int)S.exp_bytes * 2;
+
+  // The whole job is one stream of Montgomery multiplies x <- x * Y driven by a small
+  // state machine, so the multiply body is inlined exactly once (register allocation
+  // of one ~150-VGPR body instead of several).  All branches are launch-uniform.
+  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3 };
+  int phase = kBegin, k = 2, w = 0, sub = 0;
+  uint32_t o = 0, t = 0, kf = 0;
+  bool x_is_one = true;
+  const uint8_t* e = nullptr;
   if (S.has_base) {
-    const uint32_t* B = elems + (size_t)J[0] * kW;
-    // table: one, B, B^2 .. B^15
-    {
-      uint32_t one[kL];
-      load_elem(one, C->one);
-      store_elem(tbl, one);
-    }
+    uint32_t one[kL];
+    load_elem(one, C->one);
+    store_elem(tbl, one);
     load_elem(x, B);
     store_elem(tbl + kW, x);
-    elem_to_lds(slot, B);
-    wave_sync();
-#pragma unroll 1
-    for (int k = 2; k < 16; ++k) {
-      M.mul(x, slot);
-      store_elem(tbl + (size_t)k * kW, x);
-    }
-    wave_sync();
+    phase = kTable;
   }
-#pragma unroll 1
-  for (uint32_t o = 0; o < S.nout; ++o) {
-    bool x_is_one = true;
-    if (S.has_base) {
-      const uint8_t* e = scalars + (size_t)J[1 + o] * S.exp_bytes;
-      const int nwin = (int)S.exp_bytes * 2;
-      load_elem(x, tbl + (size_t)(e[0] >> 4) * kW);
-#pragma unroll 1
-      for (int w = 1; w < nwin; ++w) {
-        msqr(M, x, slot);
-        msqr(M, x, slot);
-        msqr(M, x, slot);
-        msqr(M, x, slot);
+  while (true) {
+    const uint32_t* ysrc = nullptr;  // nullptr: square
+    bool done = false;
+    while (true) {
+      if (phase == kTable) {
+        if (k < 16) { ysrc = B; break; }
+        phase = kBegin;
+        continue;
+      }
+      if (phase == kBegin) {
+        if (o >= S.nout) { done = true; break; }
+        if (S.has_base) {
+          e = scalars + (size_t)J[1 + o] * S.exp_bytes;
+          load_elem(x, tbl + (size_t)(e[0] >> 4) * kW);
+          w = 1; sub = 0; x_is_one = false;
+          phase = kVar;
+        } else {
+          x_is_one = true;
+          t = 0; kf = 0;
+          phase = kFb;
+        }
+        continue;
+      }
+      if (phase == kVar) {
+        if (w >= nwin) { t = 0; kf = 0; phase = kFb; continue; }
+        if (sub < 4) break;  // square
         const uint32_t byte = e[w >> 1];
         const uint32_t d = (w & 1) ? (byte & 15u) : (byte >> 4);
-        mmul_g(M, x, slot, tbl + (size_t)d * kW);
+        ysrc = tbl + (size_t)d * kW;
+        break;
       }
-      x_is_one = false;
-    }
-#pragma unroll 1
-    for (uint32_t t = 0; t < S.nfb[o]; ++t) {
+      // kFb
+      if (t >= S.nfb[o]) {
+        if (x_is_one) load_elem(x, C->one);
+        if (gid < njobs) store_elem(out + (size_t)J[3 + o] * kW, x);
+        ++o;
+        phase = kBegin;
+        continue;
+      }
       const FbTab& T = S.tab[o][t] ? fb1 : fb0;
-      fb_ladder(M, x, slot, T, scalars + (size_t)J[5 + 2 * o + t] * 32, x_is_one);
-      x_is_one = false;
+      if (kf >= T.nwin) { ++t; kf = 0; continue; }
+      const uint32_t d = be_digit(scalars + (size_t)J[5 + 2 * o + t] * 32, 32, kf * T.wbits, T.wbits);
+      const uint32_t* ent = T.data + ((size_t)(kf << T.wbits) + d) * kW;
+      if (x_is_one) { load_elem(x, ent); x_is_one = false; ++kf; continue; }
+      ysrc = ent;
+      break;
     }
-    if (x_is_one) load_elem(x, C->one);
-    if (gid < njobs) store_elem(out + (size_t)J[3 + o] * kW, x);
+    if (done) break;
+    // ---- the one Montgomery multiply ----
+    if (ysrc) elem_to_lds(slot, ysrc);
+    else regs_to_lds(slot, x);
+    wave_sync();
+    M.mul(x, slot);
+    wave_sync();
+    // ---- bookkeeping ----
+    if (phase == kTable) { store_elem(tbl + (size_t)k * kW, x); ++k; }
+    else if (phase == kVar) { if (++sub == 5) { sub = 0; ++w; } }
+    else { ++kf; }
   }
 }
 

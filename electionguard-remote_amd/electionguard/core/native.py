@@ -83,6 +83,8 @@ def load(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
+    if path is None and os.environ.get("EG_LIB"):
+        path = os.environ["EG_LIB"]  # A/B builds (tools/ab_mm.py); production uses the in-tree default
     p = Path(path) if path else LIB_PATH
     if not p.exists():
         raise NativeUnavailable(
