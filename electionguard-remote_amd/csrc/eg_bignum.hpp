@@ -52,6 +52,7 @@ struct MontConsts {
   uint32_t pw[128];    // p as 128 little-endian 32-bit words (final compare / subtract)
   uint32_t n0;         // -p^-1 mod 2^27
   uint32_t friendly;   // n0 == 1 (p = -1 mod 2^27): EG production group
+  uint32_t mask;       // 2^27 - 1 (read at run time so AND can fuse into DPP moves)
 };
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

@@ -367,6 +367,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   for (int i = 0; i < 6; ++i) inv *= 2u - p[0] * inv;
   c->h.n0 = (0u - inv) & kMask;
   c->h.friendly = c->h.n0 == 1 ? 1u : 0u;
+  c->h.mask = kMask;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;

@@ -12,6 +12,9 @@
 namespace eg {
 
 constexpr int kBlock = 256;
+#ifndef EG_MASK_RT
+#define EG_MASK_RT 0
+#endif
 #ifndef EG_MIN_WAVES
 #define EG_MIN_WAVES 1  // __launch_bounds__ min waves per SIMD for the Montgomery kernels
 #endif
@@ -48,7 +51,11 @@ struct Mont {
     for (int j = 0; j < kL; ++j) p[j] = s[j];
 #endif
     n0 = C->n0;
-    mask = kMask;  // (an opaque VGPR mask lets DPP+AND fuse but costs ~80 VGPRs of RA quality)
+#if EG_MASK_RT
+    mask = C->mask;  // run-time mask: lets the DPP combiner fold AND into v_and_b32_dpp
+#else
+    mask = kMask;
+#endif
   }
   __device__ __forceinline__ void mul(uint32_t (&x)[kL], const uint32_t* y) const {
     mont_mul<F>(x, y, p, n0, mask);

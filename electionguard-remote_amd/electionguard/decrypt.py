@@ -215,6 +215,8 @@ class Decryption:
         parts = []  # (n,512) arrays to multiply together
         for tr in self.trustees:
             res = tr.directDecrypt(G, T, self.qbar)
+            if len(res) != n:  # remote proxies return [] on failure (RemoteDecryptingTrusteeProxy.java:64-66)
+                raise ValueError(f"trustee {tr.id()} returned {len(res)} of {n} direct decryptions")
             ok = verify_shares(G, self.qbar, [tr.electionPublicKey()] * n, T, [r.partialDecryption for r in res],
                                [r.proof for r in res])
             if not ok.all():
@@ -223,6 +225,8 @@ class Decryption:
         for l in self.missing:
             for tr in self.trustees:
                 res = tr.compensatedDecrypt(G, l, T, self.qbar)
+                if len(res) != n:
+                    raise ValueError(f"trustee {tr.id()} returned {len(res)} of {n} compensated decryptions for {l}")
                 ok = verify_shares(G, self.qbar, [r.recoveredPublicKeyShare for r in res], T,
                                    [r.partialDecryption for r in res], [r.proof for r in res])
                 if not ok.all():

@@ -1,0 +1,278 @@
+"""Remote DecryptingTrustee over gRPC — wire-compatible with the reference.
+
+Reference: ``service DecryptingTrusteeService`` (src/main/proto/decrypting_trustee_rpc.proto:9-45)
+over the messages of src/main/proto/common.proto:8-28 and common_rpc.proto:8-14 (no
+``package`` statement, so the method paths are ``/DecryptingTrusteeService/<method>``).
+``protoc`` / ``grpc_tools`` are not in the image, so the descriptors are built here
+programmatically with the reference's message names and field numbers.
+
+* :class:`DecryptingTrusteeServer` — the trustee process (``RunRemoteDecryptingTrustee``,
+  RunRemoteDecryptingTrustee.java:58-120, handlers :180-247): each RPC is ONE GPU batch;
+  exceptions become the response ``error`` string (:200-204), never a gRPC status.
+* :class:`RemoteDecryptingTrusteeProxy` — the mediator-side ``DecryptingTrusteeIF``
+  (RemoteDecryptingTrusteeProxy.java:30-122): on an error string or a transport failure it
+  returns an EMPTY list (:64-66, :103-105), as the reference does.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from concurrent import futures
+from typing import List, Optional, Sequence
+
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+log = logging.getLogger(__name__)
+
+_F = descriptor_pb2.FieldDescriptorProto
+
+
+def _msg(fd, name, fields):
+    m = fd.message_type.add()
+    m.name = name
+    for fname, num, ftype, label, tname in fields:
+        f = m.field.add()
+        f.name, f.number, f.type, f.label = fname, num, ftype, label
+        if tname:
+            f.type_name = tname
+    return m
+
+
+def _build_pool():
+    pool = descriptor_pool.DescriptorPool()
+    opt, rep = _F.LABEL_OPTIONAL, _F.LABEL_REPEATED
+    B, S, M, BOOL, U32 = _F.TYPE_BYTES, _F.TYPE_STRING, _F.TYPE_MESSAGE, _F.TYPE_BOOL, _F.TYPE_UINT32
+    common = descriptor_pb2.FileDescriptorProto(name="common.proto", syntax="proto3")
+    _msg(common, "ElementModP", [("value", 1, B, opt, None)])
+    _msg(common, "ElementModQ", [("value", 1, B, opt, None)])
+    _msg(common, "ElGamalCiphertext", [("pad", 1, M, opt, ".ElementModP"), ("data", 2, M, opt, ".ElementModP")])
+    gp = _msg(common, "GenericChaumPedersenProof", [("challenge", 3, M, opt, ".ElementModQ"),
+                                                    ("response", 4, M, opt, ".ElementModQ")])
+    for lo in (1, 2):  # reserved 1; reserved 2;  (common.proto:24-25)
+        r = gp.reserved_range.add()
+        r.start, r.end = lo, lo + 1
+    _msg(common, "UInt256", [("value", 1, B, opt, None)])
+    pool.Add(common)
+    crpc = descriptor_pb2.FileDescriptorProto(name="common_rpc.proto", syntax="proto3")
+    _msg(crpc, "FinishRequest", [("all_ok", 1, BOOL, opt, None)])
+    _msg(crpc, "ErrorResponse", [("error", 1, S, opt, None)])
+    pool.Add(crpc)
+    dt = descriptor_pb2.FileDescriptorProto(name="decrypting_trustee_rpc.proto", syntax="proto3",
+                                            dependency=["common.proto", "common_rpc.proto"])
+    _msg(dt, "DirectDecryptionRequest", [("extended_base_hash", 1, M, opt, ".ElementModQ"),
+                                         ("text", 2, M, rep, ".ElGamalCiphertext")])
+    _msg(dt, "DirectDecryptionResponse", [("error", 1, S, opt, None),
+                                          ("results", 2, M, rep, ".DirectDecryptionResult")])
+    _msg(dt, "DirectDecryptionResult", [("decryption", 1, M, opt, ".ElementModP"),
+                                        ("proof", 2, M, opt, ".GenericChaumPedersenProof")])
+    _msg(dt, "CompensatedDecryptionRequest", [("extended_base_hash", 1, M, opt, ".ElementModQ"),
+                                              ("missing_guardian_id", 2, S, opt, None),
+                                              ("text", 3, M, rep, ".ElGamalCiphertext")])
+    _msg(dt, "CompensatedDecryptionResponse", [("error", 1, S, opt, None),
+                                               ("results", 2, M, rep, ".CompensatedDecryptionResult")])
+    _msg(dt, "CompensatedDecryptionResult", [("decryption", 1, M, opt, ".ElementModP"),
+                                             ("proof", 2, M, opt, ".GenericChaumPedersenProof"),
+                                             ("recoveryPublicKey", 3, M, opt, ".ElementModP")])
+    svc = dt.service.add()
+    svc.name = "DecryptingTrusteeService"
+    for name, req, resp in [("directDecrypt", ".DirectDecryptionRequest", ".DirectDecryptionResponse"),
+                            ("compensatedDecrypt", ".CompensatedDecryptionRequest", ".CompensatedDecryptionResponse"),
+                            ("finish", ".FinishRequest", ".ErrorResponse")]:
+        m = svc.method.add()
+        m.name, m.input_type, m.output_type = name, req, resp
+    pool.Add(dt)
+    return pool
+
+
+POOL = _build_pool()
+MSG = {name: message_factory.GetMessageClass(POOL.FindMessageTypeByName(name)) for name in [
+    "ElementModP", "ElementModQ", "ElGamalCiphertext", "GenericChaumPedersenProof", "UInt256", "FinishRequest",
+    "ErrorResponse", "DirectDecryptionRequest", "DirectDecryptionResponse", "DirectDecryptionResult",
+    "CompensatedDecryptionRequest", "CompensatedDecryptionResponse", "CompensatedDecryptionResult"]}
+SERVICE = "DecryptingTrusteeService"
+
+
+# ---- ConvertCommonProto (ConvertCommonProto.java:41-144) ----
+def publish_p(x: int):
+    return MSG["ElementModP"](value=int(x).to_bytes(512, "big"))
+
+
+def publish_q(x: int):
+    return MSG["ElementModQ"](value=int(x).to_bytes(32, "big"))
+
+
+def import_int(m) -> Optional[int]:
+    """new BigInteger(1, bytes); empty -> None (ConvertCommonProto.java:42-44, 51-53)."""
+    if m is None or len(m.value) == 0:
+        return None
+    return int.from_bytes(m.value, "big")
+
+
+def publish_ct(pad: int, data: int):
+    return MSG["ElGamalCiphertext"](pad=publish_p(pad), data=publish_p(data))
+
+
+def _texts_from(req):
+    out = []
+    for t in req.text:
+        if not t.HasField("pad"):
+            raise ValueError("ciphertext without pad")  # importCiphertext returns null (:60-62)
+        out.append((import_int(t.pad), import_int(t.data)))
+    return out
+
+
+class DecryptingTrusteeServer:
+    """gRPC DecryptingTrusteeService backed by a GPU DecryptingTrustee (one GPU per process)."""
+
+    def __init__(self, group, trustee, port: int = 0, host: str = "127.0.0.1", max_workers: int = 4):
+        import grpc
+
+        self.group, self.trustee = group, trustee
+        self._done = threading.Event()
+        self.all_ok: Optional[bool] = None
+        handlers = {
+            "directDecrypt": grpc.unary_unary_rpc_method_handler(
+                self._direct, request_deserializer=MSG["DirectDecryptionRequest"].FromString,
+                response_serializer=MSG["DirectDecryptionResponse"].SerializeToString),
+            "compensatedDecrypt": grpc.unary_unary_rpc_method_handler(
+                self._compensated, request_deserializer=MSG["CompensatedDecryptionRequest"].FromString,
+                response_serializer=MSG["CompensatedDecryptionResponse"].SerializeToString),
+            "finish": grpc.unary_unary_rpc_method_handler(
+                self._finish, request_deserializer=MSG["FinishRequest"].FromString,
+                response_serializer=MSG["ErrorResponse"].SerializeToString),
+        }
+        # default 4 MiB inbound cap as the reference channel; raise for large tallies
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
+                                  options=[("grpc.max_receive_message_length", 256 << 20),
+                                           ("grpc.max_send_message_length", 256 << 20)])
+        self.server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
+        self.port = self.server.add_insecure_port(f"{host}:{port}")
+
+    def start(self) -> "DecryptingTrusteeServer":
+        self.server.start()
+        return self
+
+    def wait(self, timeout: Optional[float] = None) -> bool:
+        return self._done.wait(timeout)
+
+    def stop(self) -> None:
+        self.server.stop(grace=1).wait()
+
+    # RunRemoteDecryptingTrustee.directDecrypt (:180-208)
+    def _direct(self, req, ctx):
+        resp = MSG["DirectDecryptionResponse"]()
+        try:
+            texts = _texts_from(req)
+            qbar = import_int(req.extended_base_hash)
+            res = self.trustee.directDecrypt(self.group, texts, qbar, None)
+            for r in res:
+                resp.results.add(decryption=publish_p(r.partialDecryption),
+                                 proof=MSG["GenericChaumPedersenProof"](challenge=publish_q(r.proof.c),
+                                                                        response=publish_q(r.proof.v)))
+        except Exception as e:  # error string, not a gRPC status (:200-204)
+            log.exception("directDecrypt failed")
+            del resp.results[:]
+            resp.error = str(e) or "Unknown"
+        return resp
+
+    # RunRemoteDecryptingTrustee.compensatedDecrypt (:217-247)
+    def _compensated(self, req, ctx):
+        resp = MSG["CompensatedDecryptionResponse"]()
+        try:
+            texts = _texts_from(req)
+            qbar = import_int(req.extended_base_hash)
+            res = self.trustee.compensatedDecrypt(self.group, req.missing_guardian_id, texts, qbar, None)
+            for r in res:
+                resp.results.add(decryption=publish_p(r.partialDecryption),
+                                 proof=MSG["GenericChaumPedersenProof"](challenge=publish_q(r.proof.c),
+                                                                        response=publish_q(r.proof.v)),
+                                 recoveryPublicKey=publish_p(r.recoveredPublicKeyShare))
+        except Exception as e:
+            log.exception("compensatedDecrypt failed")
+            del resp.results[:]
+            resp.error = str(e) or "Unknown"
+        return resp
+
+    def _finish(self, req, ctx):
+        self.all_ok = bool(req.all_ok)
+        self._done.set()
+        return MSG["ErrorResponse"]()
+
+
+class RemoteDecryptingTrusteeProxy:
+    """Mediator-side DecryptingTrusteeIF over gRPC (RemoteDecryptingTrusteeProxy.java)."""
+
+    def __init__(self, trustee_id: str, url: str, x: int, public_key: int):
+        import grpc
+
+        self._id, self._x, self._K = trustee_id, x, public_key
+        self.channel = grpc.insecure_channel(url, options=[("grpc.max_receive_message_length", 256 << 20),
+                                                           ("grpc.max_send_message_length", 256 << 20),
+                                                           ("grpc.keepalive_time_ms", 60000)])
+        mk = lambda m, req, resp: self.channel.unary_unary(f"/{SERVICE}/{m}", request_serializer=req.SerializeToString,
+                                                           response_deserializer=resp.FromString)
+        self._direct = mk("directDecrypt", MSG["DirectDecryptionRequest"], MSG["DirectDecryptionResponse"])
+        self._comp = mk("compensatedDecrypt", MSG["CompensatedDecryptionRequest"], MSG["CompensatedDecryptionResponse"])
+        self._finish = mk("finish", MSG["FinishRequest"], MSG["ErrorResponse"])
+
+    def id(self) -> str:
+        return self._id
+
+    def xCoordinate(self) -> int:
+        return self._x
+
+    def electionPublicKey(self) -> int:
+        return self._K
+
+    def directDecrypt(self, group, texts, extendedBaseHash: int, nonce=None):
+        import grpc
+        from .decrypt import DirectDecryptionAndProof, GenericChaumPedersenProof, _texts_array
+
+        T = _texts_array(texts)
+        req = MSG["DirectDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash),
+                                             text=[publish_ct(int.from_bytes(t[0].tobytes(), "big"),
+                                                              int.from_bytes(t[1].tobytes(), "big")) for t in T])
+        try:
+            resp = self._direct(req)
+        except grpc.RpcError as e:
+            log.error("directDecrypt failed: %s", e)
+            return []
+        if resp.error:
+            log.error("directDecrypt failed: %s", resp.error)
+            return []
+        return [DirectDecryptionAndProof(import_int(r.decryption),
+                                         GenericChaumPedersenProof(import_int(r.proof.challenge),
+                                                                   import_int(r.proof.response)))
+                for r in resp.results]
+
+    def compensatedDecrypt(self, group, missingGuardianId: str, texts, extendedBaseHash: int, nonce=None):
+        import grpc
+        from .decrypt import CompensatedDecryptionAndProof, GenericChaumPedersenProof, _texts_array
+
+        T = _texts_array(texts)
+        req = MSG["CompensatedDecryptionRequest"](
+            extended_base_hash=publish_q(extendedBaseHash), missing_guardian_id=missingGuardianId,
+            text=[publish_ct(int.from_bytes(t[0].tobytes(), "big"), int.from_bytes(t[1].tobytes(), "big")) for t in T])
+        try:
+            resp = self._comp(req)
+        except grpc.RpcError as e:
+            log.error("compensatedDecrypt failed: %s", e)
+            return []
+        if resp.error:
+            log.error("compensatedDecrypt failed: %s", resp.error)
+            return []
+        return [CompensatedDecryptionAndProof(import_int(r.decryption),
+                                              GenericChaumPedersenProof(import_int(r.proof.challenge),
+                                                                        import_int(r.proof.response)),
+                                              import_int(r.recoveryPublicKey)) for r in resp.results]
+
+    def finish(self, all_ok: bool) -> str:
+        import grpc
+
+        try:
+            return self._finish(MSG["FinishRequest"](all_ok=all_ok)).error
+        except grpc.RpcError as e:
+            return str(e)
+
+    def close(self) -> None:
+        self.channel.close()
