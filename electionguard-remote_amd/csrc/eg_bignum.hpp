@@ -81,6 +81,48 @@ __device__ __forceinline__ uint32_t bcast_g0(uint32_t v) {
 #endif
 }
 
+#ifndef EG_ASM_DPP
+#define EG_ASM_DPP 0  // 1: AND fused into the DPP moves by inline asm (v_and_b32_dpp)
+#endif
+
+// (v & mask) of group-lane 0, broadcast to the group  (fused form)
+__device__ __forceinline__ uint32_t bcast_g0_and(uint32_t v, uint32_t mask) {
+#if EG_ASM_DPP && EG_BCAST == 0
+  uint32_t r;
+  // s_nop 1: a VALU-written VGPR read through DPP needs 2 wait states
+  if constexpr (kT == 8) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_and_b32_dpp %0, %1, %2 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_mov_b32_dpp %0, %0 row_shr:4 row_mask:0xf bank_mask:0xa"
+        : "=&v"(r) : "v"(v), "v"(mask));
+  } else {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_and_b32_dpp %0, %1, %2 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf"
+        : "=v"(r) : "v"(v), "v"(mask));
+  }
+  return r;
+#else
+  return bcast_g0(v) & mask;
+#endif
+}
+
+// (v & mask) from lane+1 within the DPP row (0 at the row end)  (fused form)
+__device__ __forceinline__ uint32_t from_next_and(uint32_t v, uint32_t mask) {
+#if EG_ASM_DPP
+  uint32_t r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_and_b32_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "=v"(r) : "v"(v), "v"(mask));
+  return r;
+#else
+  return __builtin_amdgcn_mov_dpp(v, 0x101 /*row_shl:1*/, 0xF, 0xF, true) & mask;
+#endif
+}
+
 // value from lane+1 within the DPP row (0 at the row end)
 __device__ __forceinline__ uint32_t from_next(uint32_t v) {
   return __builtin_amdgcn_mov_dpp(v, 0x101 /*row_shl:1*/, 0xF, 0xF, true);
@@ -117,7 +159,7 @@ __device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __re
       // quotient digit from the group's lowest limb
       uint32_t t0 = (uint32_t)acc[r % kL];
       if constexpr (!FRIENDLY) t0 *= n0;
-      const uint32_t m = bcast_g0(t0) & mask;
+      const uint32_t m = bcast_g0_and(t0, mask);
       // t += m * p
 #pragma unroll
       for (int j = 0; j < kL; ++j) {
@@ -128,7 +170,7 @@ __device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __re
       // low 27 bits shift into lane-1's top position (0 for the group's lane 0)
       uint64_t& A0 = acc[r % kL];
       acc[(r + 1) % kL] += A0 >> kLimbBits;
-      A0 = (uint64_t)(from_next((uint32_t)A0) & mask);
+      A0 = (uint64_t)from_next_and((uint32_t)A0, mask);
     }
   }
   // two parallel carry passes -> limbs < 2^27 + 2^11 (enough headroom for the next op)

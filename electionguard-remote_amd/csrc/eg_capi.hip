@@ -13,6 +13,7 @@
 #pragma clang diagnostic ignored "-Wunused-result"
 #pragma clang diagnostic ignored "-Wunused-value"
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -140,6 +141,7 @@ struct eg_ctx {
   std::vector<ProfRec> prof;
   uint8_t K_be[512];
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
+  uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
 };
 static std::vector<ProfRec>& prof_of(eg_ctx* c) { return c->prof; }
 
@@ -186,11 +188,12 @@ static int launch_export(eg_ctx* c, const uint32_t* d_in, size_t n, uint8_t* d_b
 
 // Algorithmic Montgomery multiplications of one k_pow job (mirrors the kernel).
 static double pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
-  double mm = S.has_base ? 14.0 : 0.0;
+  double mm = 0;
+  if (S.has_base) mm = S.comb ? (double)((kCombH - 1) * kCombW + ((1 << kCombH) - kCombH - 1)) : 14.0;
   for (uint32_t o = 0; o < S.nout; ++o) {
     bool one = true;
     if (S.has_base) {
-      mm += (double)(S.exp_bytes * 2 - 1) * 5.0;
+      mm += S.comb ? (double)(kCombW - 1) * 2.0 : (double)(S.exp_bytes * 2 - 1) * 5.0;
       one = false;
     }
     for (uint32_t t = 0; t < S.nfb[o]; ++t) {
@@ -208,7 +211,7 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
                       const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1) {
   if (!njobs) return EG_OK;
   uint32_t* scr = nullptr;
-  const size_t per = S.has_base ? (size_t)16 * kW * 4 : 4;
+  const size_t per = S.has_base ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
   // bound the per-launch scratch (table of 16 powers per job)
   const size_t max_jobs = (size_t)1 << 18;
   const double mm_job = pow_job_mm(S, f0, f1);
@@ -314,8 +317,8 @@ static int import_one(eg_ctx* c, const uint8_t be[512], uint32_t** d_mont_out) {
 }
 
 static int fb_create_locked(eg_ctx* c, const uint8_t base_be[512], int wbits, eg_fixed_base** out) {
-  if (!(wbits == 4 || wbits == 8 || wbits == 11 || wbits == 12 || wbits == 16))
-    return fail(EG_ERR_ARG, "window_bits must be 4, 8, 11, 12 or 16");
+  if (wbits < 4 || wbits > 22)
+    return fail(EG_ERR_ARG, "window_bits must be in [4, 22]");
   uint32_t* d_m = nullptr;
   int rc = import_one(c, base_be, &d_m);
   if (rc) return rc;
@@ -368,6 +371,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   c->h.n0 = (0u - inv) & kMask;
   c->h.friendly = c->h.n0 == 1 ? 1u : 0u;
   c->h.mask = kMask;
+  if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;

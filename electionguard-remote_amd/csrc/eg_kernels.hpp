@@ -226,7 +226,12 @@ constexpr int kJobWords = 9;
 struct PowShape {
   uint32_t has_base, nout, nfb[2], tab[2][2];
   uint32_t exp_bytes;  // variable-base exponent length (32, or 512 for inverses)
+  uint32_t comb;       // 1: Lim-Lee comb (h = 5) shared by the job's exponents (32-byte only)
 };
+
+// Lim-Lee comb parameters for 256-bit exponents: 5 rows of 52 bits.
+constexpr int kCombH = 5;
+constexpr int kCombW = 52;
 
 __device__ __forceinline__ uint32_t be_digit(const uint8_t* __restrict__ e, int nbytes, int bit, int wb) {
   uint32_t v = 0;
@@ -263,21 +268,28 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
                                                 const uint8_t* __restrict__ scalars,
                                                 uint32_t* __restrict__ out, uint32_t* __restrict__ scratch,
                                                 FbTab fb0, FbTab fb1) {
+  __shared__ uint8_t s_dig[kGroupsPerBlock][64];
   const uint32_t gid = group_id();
   const uint32_t jb = gid < njobs ? gid : njobs - 1;
   const uint32_t* J = jobs + (size_t)jb * kJobWords;
   uint32_t* slot = group_slot();
+  uint8_t* dig = s_dig[threadIdx.x / kT];
   Mont<F> M;
   M.load(C);
   uint32_t x[kL];
-  uint32_t* tbl = scratch + (size_t)gid * 16 * kW;
+  const bool comb = S.comb != 0;
+  const uint32_t tsize = comb ? (1u << kCombH) : 16u;
+  uint32_t* tbl = scratch + (size_t)gid * tsize * kW;
   const uint32_t* B = S.has_base ? elems + (size_t)J[0] * kW : nullptr;
   const int nwin = (int)S.exp_bytes * 2;
 
   // The whole job is one stream of Montgomery multiplies x <- x * Y driven by a small
   // state machine, so the multiply body is inlined exactly once (register allocation
   // of one ~150-VGPR body instead of several).  All branches are launch-uniform.
-  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3 };
+  //   window path: table B^0..B^15 (14 MM), per exponent 63 x (4 sq + 1 mul)
+  //   comb path  : y_k = B^(2^(52k)) (208 sq), table of the 32 subset products (26 MM),
+  //                per exponent 51 x (1 sq + 1 mul) from column digits
+  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3, kPre = 4, kCTab = 5, kComb = 6 };
   int phase = kBegin, k = 2, w = 0, sub = 0;
   uint32_t o = 0, t = 0, kf = 0;
   bool x_is_one = true;
@@ -288,12 +300,26 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     store_elem(tbl, one);
     load_elem(x, B);
     store_elem(tbl + kW, x);
-    phase = kTable;
+    phase = comb ? kPre : kTable;
+    k = comb ? 0 : 2;
   }
   while (true) {
     const uint32_t* ysrc = nullptr;  // nullptr: square
     bool done = false;
     while (true) {
+      if (phase == kPre) {  // k squarings done so far
+        if (k < (kCombH - 1) * kCombW) break;  // square
+        phase = kCTab;
+        k = 3;
+        continue;
+      }
+      if (phase == kCTab) {  // entry k = (k & (k-1)) * (lowest bit of k)
+        while (k < (1 << kCombH) && (k & (k - 1)) == 0) ++k;
+        if (k >= (1 << kCombH)) { phase = kBegin; continue; }
+        load_elem(x, tbl + (size_t)(k & (k - 1)) * kW);
+        ysrc = tbl + (size_t)(k & -k) * kW;
+        break;
+      }
       if (phase == kTable) {
         if (k < 16) { ysrc = B; break; }
         phase = kBegin;
@@ -303,15 +329,40 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         if (o >= S.nout) { done = true; break; }
         if (S.has_base) {
           e = scalars + (size_t)J[1 + o] * S.exp_bytes;
-          load_elem(x, tbl + (size_t)(e[0] >> 4) * kW);
-          w = 1; sub = 0; x_is_one = false;
-          phase = kVar;
+          x_is_one = false;
+          if (comb) {
+            // column digits: bit j of each of the 5 rows (52 bits each)
+            wave_sync();
+            for (int j = glane(); j < kCombW; j += kT) {
+              uint32_t d = 0;
+#pragma unroll
+              for (int r = 0; r < kCombH; ++r) {
+                const int bit = r * kCombW + j;
+                if (bit < 256) d |= (((uint32_t)e[31 - (bit >> 3)] >> (bit & 7)) & 1u) << r;
+              }
+              dig[j] = (uint8_t)d;
+            }
+            wave_sync();
+            load_elem(x, tbl + (size_t)dig[kCombW - 1] * kW);
+            w = kCombW - 2; sub = 0;
+            phase = kComb;
+          } else {
+            load_elem(x, tbl + (size_t)(e[0] >> 4) * kW);
+            w = 1; sub = 0;
+            phase = kVar;
+          }
         } else {
           x_is_one = true;
           t = 0; kf = 0;
           phase = kFb;
         }
         continue;
+      }
+      if (phase == kComb) {
+        if (w < 0) { t = 0; kf = 0; phase = kFb; continue; }
+        if (sub == 0) break;  // square
+        ysrc = tbl + (size_t)dig[w] * kW;
+        break;
       }
       if (phase == kVar) {
         if (w >= nwin) { t = 0; kf = 0; phase = kFb; continue; }
@@ -347,6 +398,12 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     // ---- bookkeeping ----
     if (phase == kTable) { store_elem(tbl + (size_t)k * kW, x); ++k; }
     else if (phase == kVar) { if (++sub == 5) { sub = 0; ++w; } }
+    else if (phase == kPre) {
+      ++k;
+      if (k % kCombW == 0) store_elem(tbl + ((size_t)1 << (k / kCombW)) * kW, x);
+    }
+    else if (phase == kCTab) { store_elem(tbl + (size_t)k * kW, x); ++k; }
+    else if (phase == kComb) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
     else { ++kf; }
   }
 }

@@ -78,7 +78,8 @@ int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_muls, int* l
 eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
 
 /* Fixed-base radix table (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit
- * windows).  window_bits in {4, 8, 11, 16}; table = ceil(256/w) * 2^w elements. */
+ * windows).  window_bits in [4, 22]; table = ceil(256/w) * 2^w elements of 640 B
+ * in HBM (w = 16: 671 MB, w = 22: 32 GB). */
 int eg_fixed_base_create(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], int window_bits,
                          eg_fixed_base** out);
 int eg_fixed_base_destroy(eg_fixed_base* fb);
