@@ -63,7 +63,7 @@ __device__ __forceinline__ int gslot() { return lane_id() / kT; }        // grou
 #define EG_BCAST 0  // 0: DPP (VALU), 1: ds_swizzle (LDS pipe, no VALU issue slot)
 #endif
 #ifndef EG_PLDS
-#define EG_PLDS 0   // 1: modulus limbs read from LDS instead of VGPRs
+#define EG_PLDS 1   // 1: modulus limbs read from LDS instead of VGPRs (frees 19 VGPRs: 3 waves/SIMD)
 #endif
 
 // Broadcast group-lane 0's value to the whole group.
