@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--ballots", type=int, default=10000, help="ballots per GPU")
     ap.add_argument("--contests", type=int, default=4)
     ap.add_argument("--selections", type=int, default=5)
-    ap.add_argument("--fb-window", type=int, default=16, help="fixed-base radix window bits for g and K")
+    ap.add_argument("--fb-window", type=int, default=22, help="fixed-base radix window bits for g and K")
     ap.add_argument("--cpu-sample", type=int, default=256, help="ballots for the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
