@@ -24,7 +24,6 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "electionguard-remote_amd"))
 
-MAC_PER_MM = 2 * 128 * 128   # algorithmic u32xu32 MACs per 4096-bit Montgomery multiply
 PEAK_TMAC = 256 * 64 * 2.4e9 / 1e12   # 256 CUs x 64 v_mad_u64_u32 lanes/clk/CU x 2.4 GHz (profiles/r01_ubench_isa.txt)
 
 
@@ -115,7 +114,8 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    kms, kmm, klaunch = group.profile_end()
+    kp = group.profile_end()
+    kms, kmm, klaunch = kp.ms, kp.mont_ops, kp.launches
     if dist:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -123,8 +123,9 @@ def main():
 
     total_ballots = nb * world * a.steps
     value = total_ballots / el
-    # algorithmic work of the dominant kernel (k_pow), from its own launch schedule
-    achieved = kmm * MAC_PER_MM / (kms / 1e3) / 1e12 if kms > 0 else None
+    # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
+    # 2*128^2 u32 MACs per multiply, 128*129/2 + 128^2 per squaring (group.MAC_PER_*)
+    achieved = kp.macs / (kms / 1e3) / 1e12 if kms > 0 else None
     mm_per_ballot = kmm / (nb * a.steps) if a.steps else None
     out = {
         "metric": "ballots verified+tallied/sec (node, 4096-bit group)",
@@ -158,18 +159,23 @@ def main():
             "traffic": None,
             "kernel_ms_per_launch": round(kms / max(klaunch, 1), 3),
             "launches": klaunch,
-            "mont_mul_per_launch": round(kmm / max(klaunch, 1)),
+            "mont_ops_per_launch": round(kmm / max(klaunch, 1)),
+            "squaring_frac": round(kp.squarings / kmm, 4) if kmm else None,
         },
-        "mont_mul_per_ballot": round(mm_per_ballot, 1) if mm_per_ballot else None,
+        "mont_ops_per_ballot": round(mm_per_ballot, 1) if mm_per_ballot else None,
         "modexp_per_s_per_gpu": round((104 + 132) * value / world, 1),
         "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
     }
+    # HBM traffic of k_pow from the committed PMC passes of this same command
+    # (tools/profile_round.sh); only quoted when the profiled workload matches this run's.
     prof = ROOT / "profiles" / "r01_pmc_kpow.json"
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
-            out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-        except Exception:
+            if pm.get("bench_config") == out["config"]:
+                out["roofline"]["traffic"] = round(pm["traffic"]["hbm_bytes_per_launch"])
+                out["roofline"]["traffic_source"] = "profiles/r01_pmc_kpow.json"
+        except (KeyError, ValueError, TypeError):
             pass
 
     if rank == 0 and world == 1 and a.cpu_sample > 0:

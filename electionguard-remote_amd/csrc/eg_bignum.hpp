@@ -135,26 +135,63 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t v) {
 // Montgomery multiply  x <- x * y * R^-1 mod p  (result < 2p, limbs < 2^27 + 2^11).
 //   x : this lane's L limbs (in/out), any value < 2p, limbs <= 2^27 + 2^11
 //   y : the group's LDS slot (kW words, device element format), value < 2p
-//   p : this lane's L modulus limbs
-// CIOS, one radix-2^27 digit of y per step; 2L v_mad_u64_u32 + ~5 VALU per step.
-template <bool FRIENDLY, class PT>
-__device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
-                                         const PT& p, uint32_t n0, uint32_t mask) {
+//   p : this lane's L modulus limbs (VGPRs or LDS)
+// CIOS, one radix-2^27 digit of y per step; 2L v_mad_u64_u32 + ~7 VALU per step.
+//
+// SQR = true computes x^2 with y == x (the slot must hold x): the x*x part of each step
+// uses the symmetric half.  Pair {a, b} of limb indices (register indices ja, jb) is
+// added once, doubled, at the row whose register index is cyclically 1..9 behind the
+// other ((jb - ja) mod 19 in [1, 9] -> row a); pairs with ja == jb go to the smaller
+// index and the diagonal x_a^2 once.  At row i (register r = i mod 19, outer block s) every
+// lane therefore touches the SAME 10 register indices r..r+9 (mod 19): 9 doubled products
+// from 2x held in registers, and the diagonal register whose multiplier is
+// 2x_r (lanes > s), x_r (lane s) or 0 (lanes < s) -- one v_bfe_u32 with per-lane
+// (offset, width).  10 MACs + 1 VALU instead of 19 MACs per step.  All contributions
+// to column c still arrive by step c (each pair is added at row <= c), so the CIOS
+// quotient digits are unchanged.
+template <bool FRIENDLY, bool SQR, class PT>
+__device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
+                                              const PT& p, uint32_t n0, uint32_t mask) {
+  static_assert(!SQR || kL == 19, "symmetric schedule is written for 19 limbs per lane");
   uint64_t acc[kL];
 #pragma unroll
   for (int j = 0; j < kL; ++j) acc[j] = 0;
+  if constexpr (SQR) {
+#pragma unroll
+    for (int j = 0; j < kL; ++j) x[j] <<= 1;  // 2x < 2^29
+  }
 
 #pragma unroll 1
   for (int s = 0; s < kT; ++s) {
     const uint32_t* ys = y + s * kLP;
+    uint32_t doff = 0, dwid = 0;
+    if constexpr (SQR) {
+      const int gl = glane();
+      doff = (gl == s) ? 1u : 0u;   // own row: x_r = (2x_r) >> 1
+      dwid = (gl >= s) ? 30u : 0u;  // rows above: 2x_r; rows below: 0 (width 0)
+    }
 #pragma unroll
     for (int r = 0; r < kL; ++r) {
       const uint32_t yi = ys[r];
       // t += x * y_i     (logical position j lives in register (j + r) % L)
+      if constexpr (SQR) {
+        {
+          const uint32_t d = __builtin_amdgcn_ubfe(x[r], doff, dwid);
+          uint64_t& A = acc[(r + r) % kL];
+          A = (uint64_t)d * yi + A;
+        }
 #pragma unroll
-      for (int j = 0; j < kL; ++j) {
-        uint64_t& A = acc[(j + r) % kL];
-        A = (uint64_t)x[j] * yi + A;
+        for (int jj = 1; jj <= (kL - 1) / 2; ++jj) {
+          const int j = (r + jj) % kL;
+          uint64_t& A = acc[(j + r) % kL];
+          A = (uint64_t)x[j] * yi + A;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kL; ++j) {
+          uint64_t& A = acc[(j + r) % kL];
+          A = (uint64_t)x[j] * yi + A;
+        }
       }
       // quotient digit from the group's lowest limb
       uint32_t t0 = (uint32_t)acc[r % kL];
@@ -192,6 +229,12 @@ __device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __re
       x[j] = ((uint32_t)d[j] & mask) + c;
     }
   }
+}
+
+template <bool FRIENDLY, class PT>
+__device__ __forceinline__ void mont_mul(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
+                                         const PT& p, uint32_t n0, uint32_t mask) {
+  mont_mul_impl<FRIENDLY, false>(x, y, p, n0, mask);
 }
 
 // ---- element I/O between VGPRs, LDS slots and the device element format ----

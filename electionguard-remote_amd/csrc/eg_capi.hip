@@ -110,7 +110,8 @@ struct DevBuf {
 
 struct ProfRec {
   hipEvent_t a, b;
-  double mm;
+  double mm;   // Montgomery operations (multiplies + squarings)
+  double sqr;  // of which squarings (symmetric-half schedule)
 };
 
 struct eg_fixed_base {
@@ -186,23 +187,40 @@ static int launch_export(eg_ctx* c, const uint32_t* d_in, size_t n, uint8_t* d_b
   return EG_OK;
 }
 
-// Algorithmic Montgomery multiplications of one k_pow job (mirrors the kernel).
-static double pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
-  double mm = 0;
-  if (S.has_base) mm = S.comb ? (double)((kCombH - 1) * kCombW + ((1 << kCombH) - kCombH - 1)) : 14.0;
+// Montgomery operations of one k_pow job, split into squarings and multiplies
+// (mirrors the kernel's state machine: kPre / kComb-even / kVar sub<4 steps square).
+struct MMCount {
+  double mul = 0, sqr = 0;
+};
+static MMCount pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
+  MMCount n;
+  if (S.has_base) {
+    if (S.comb) {
+      n.sqr += (double)((kCombH - 1) * kCombW);
+      n.mul += (double)((1 << kCombH) - kCombH - 1);
+    } else {
+      n.mul += 14.0;
+    }
+  }
   for (uint32_t o = 0; o < S.nout; ++o) {
     bool one = true;
     if (S.has_base) {
-      mm += S.comb ? (double)(kCombW - 1) * 2.0 : (double)(S.exp_bytes * 2 - 1) * 5.0;
+      const double steps = S.comb ? (double)(kCombW - 1) : (double)(S.exp_bytes * 2 - 1);
+      n.sqr += steps * (S.comb ? 1.0 : 4.0);
+      n.mul += steps;
       one = false;
     }
     for (uint32_t t = 0; t < S.nfb[o]; ++t) {
       const FbTab& T = S.tab[o][t] ? f1 : f0;
-      mm += (double)T.nwin - (one ? 1.0 : 0.0);
+      n.mul += (double)T.nwin - (one ? 1.0 : 0.0);
       one = false;
     }
   }
-  return mm;
+#if !EG_SQR
+  n.mul += n.sqr;  // squarings run the plain multiply schedule
+  n.sqr = 0;
+#endif
+  return n;
 }
 
 
@@ -214,12 +232,12 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   const size_t per = S.has_base ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
   // bound the per-launch scratch (table of 16 powers per job)
   const size_t max_jobs = (size_t)1 << 18;
-  const double mm_job = pow_job_mm(S, f0, f1);
+  const MMCount mm_job = pow_job_mm(S, f0, f1);
   for (size_t off = 0; off < njobs; off += max_jobs) {
     const size_t nj = std::min(max_jobs, njobs - off);
     int rc = ws_get(c, W_SCR, padded_groups(nj) * per, (void**)&scr);
     if (rc) return rc;
-    ProfRec pr{nullptr, nullptr, mm_job * (double)nj};
+    ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj, mm_job.sqr * (double)nj};
     if (c->timing) {
       HIPCHK(hipEventCreate(&pr.a));
       HIPCHK(hipEventCreate(&pr.b));
@@ -581,22 +599,24 @@ extern "C" int eg_ctx_profile_begin(eg_ctx* c) {
   return EG_OK;
 }
 
-extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, int* launches) {
+extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr, int* launches) {
   if (!c) return fail(EG_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  double t = 0, m = 0;
+  double t = 0, m = 0, sq = 0;
   for (auto& r : c->prof) {
     float x = 0;
     HIPCHK(hipEventElapsedTime(&x, r.a, r.b));
     t += x;
     m += r.mm;
+    sq += r.sqr;
     hipEventDestroy(r.a);
     hipEventDestroy(r.b);
   }
   if (ms) *ms = t;
   if (mm) *mm = m;
+  if (sqr) *sqr = sq;
   if (launches) *launches = (int)c->prof.size();
   c->prof.clear();
   c->timing = false;

@@ -12,6 +12,9 @@
 namespace eg {
 
 constexpr int kBlock = 256;
+#ifndef EG_SQR
+#define EG_SQR 1  // squarings use the symmetric-half CIOS (eg_bignum.hpp)
+#endif
 #ifndef EG_MASK_RT
 #define EG_MASK_RT 0
 #endif
@@ -58,7 +61,15 @@ struct Mont {
 #endif
   }
   __device__ __forceinline__ void mul(uint32_t (&x)[kL], const uint32_t* y) const {
-    mont_mul<F>(x, y, p, n0, mask);
+    mont_mul_impl<F, false>(x, y, p, n0, mask);
+  }
+  // x <- x^2 (the slot must hold x); symmetric-half schedule (EG_SQR) or plain CIOS
+  __device__ __forceinline__ void sqr(uint32_t (&x)[kL], const uint32_t* y) const {
+#if EG_SQR
+    mont_mul_impl<F, true>(x, y, p, n0, mask);
+#else
+    mont_mul_impl<F, false>(x, y, p, n0, mask);
+#endif
   }
 };
 
@@ -75,7 +86,7 @@ template <bool F>
 __device__ __forceinline__ void msqr(const Mont<F>& M, uint32_t (&x)[kL], uint32_t* slot) {
   regs_to_lds(slot, x);
   wave_sync();
-  M.mul(x, slot);
+  M.sqr(x, slot);
   wave_sync();
 }
 // x <- x * E  (E a device element in global memory)
@@ -389,11 +400,16 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       break;
     }
     if (done) break;
-    // ---- the one Montgomery multiply ----
-    if (ysrc) elem_to_lds(slot, ysrc);
-    else regs_to_lds(slot, x);
-    wave_sync();
-    M.mul(x, slot);
+    // ---- the one Montgomery multiply (or square) ----
+    if (ysrc) {
+      elem_to_lds(slot, ysrc);
+      wave_sync();
+      M.mul(x, slot);
+    } else {
+      regs_to_lds(slot, x);
+      wave_sync();
+      M.sqr(x, slot);
+    }
     wave_sync();
     // ---- bookkeeping ----
     if (phase == kTable) { store_elem(tbl + (size_t)k * kW, x); ++k; }

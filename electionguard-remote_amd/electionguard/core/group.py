@@ -58,6 +58,25 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+# Algorithmic 32-bit MACs of one 4096-bit (128-word) Montgomery operation:
+# product 128^2 (a square needs only 128*129/2) + reduction 128^2.
+MAC_PER_MUL = 2 * 128 * 128
+MAC_PER_SQR = 128 * 129 // 2 + 128 * 128
+
+
+@dataclass
+class KernelProfile:
+    """Device time and work of the k_pow launches between profile_begin / profile_end."""
+    ms: float          # summed HIP-event milliseconds on the ctx stream
+    mont_ops: float    # Montgomery multiplies + squarings
+    squarings: float   # of which squarings
+    launches: int
+
+    @property
+    def macs(self) -> float:
+        return (self.mont_ops - self.squarings) * MAC_PER_MUL + self.squarings * MAC_PER_SQR
+
+
 class GroupContext:
     """GPU-backed GroupContext (one per device; calls are thread-safe)."""
 
@@ -179,11 +198,12 @@ class GroupContext:
     def profile_begin(self) -> None:
         native.check(self._lib, "eg_ctx_profile_begin", self._lib.eg_ctx_profile_begin(self._ctx))
 
-    def profile_end(self):
-        ms, mm, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    def profile_end(self) -> "KernelProfile":
+        ms, mm, sq, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         native.check(self._lib, "eg_ctx_profile_end",
-                     self._lib.eg_ctx_profile_end(self._ctx, ctypes.byref(ms), ctypes.byref(mm), ctypes.byref(n)))
-        return ms.value, mm.value, n.value
+                     self._lib.eg_ctx_profile_end(self._ctx, ctypes.byref(ms), ctypes.byref(mm), ctypes.byref(sq),
+                                                  ctypes.byref(n)))
+        return KernelProfile(ms.value, mm.value, sq.value, n.value)
 
     def sync(self) -> None:
         native.check(self._lib, "eg_ctx_sync", self._lib.eg_ctx_sync(self._ctx))

@@ -56,7 +56,7 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_ctx_destroy": ([P], I),
         "eg_ctx_sync": ([P], I),
         "eg_ctx_profile_begin": ([P], I),
-        "eg_ctx_profile_end": ([P, D, D, ctypes.POINTER(I)], I),
+        "eg_ctx_profile_end": ([P, D, D, D, ctypes.POINTER(I)], I),
         "eg_ctx_g_table": ([P], P),
         "eg_fixed_base_create": ([P, P, I, ctypes.POINTER(c_vp)], I),
         "eg_fixed_base_destroy": ([P], I),

@@ -70,10 +70,12 @@ int eg_ctx_sync(eg_ctx* ctx);
 /* Kernel-level timing of the dominant kernel (k_pow, the windowed exponentiation):
  * between begin and end every k_pow launch on the ctx stream is bracketed by HIP
  * events; end synchronises and returns the summed device milliseconds, the
- * algorithmic Montgomery multiplications those launches performed, and the
- * number of launches. */
+ * Montgomery operations those launches performed (multiplies + squarings), how
+ * many of them were squarings (which use the symmetric-half schedule, 24,640
+ * instead of 32,768 algorithmic 32-bit MACs), and the number of launches.
+ * Any out pointer may be NULL. */
 int eg_ctx_profile_begin(eg_ctx* ctx);
-int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_muls, int* launches);
+int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_ops, double* squarings, int* launches);
 /* Fixed-base table for g (built at ctx creation) — accessor. */
 eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
 
