@@ -121,6 +121,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
+    from electionguard.core import native
+    radix = native.version().split("radix2^")[1].split()[0]
     total_ballots = nb * world * a.steps
     value = total_ballots / el
     # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
@@ -138,7 +140,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32xu32->u64 (radix-2^27 limbs)",
+        "dtype": f"u32xu32->u64 (radix-2^{radix} limbs)",
         "data": "synthetic (seeded random one-hot ballots, GPU-encrypted with random nonces)",
         "config": {
             "workload": f"configs[1]: verify + homomorphic tally of {nb} ballots per GPU, "

@@ -6,11 +6,14 @@
 // integers mod p, i.e. identical to java.math.BigInteger.modPow / multiply+mod.
 //
 // Representation (MI355X-first):
-//   * radix 2^27, N = 152 limbs (4104 bits), Montgomery R = 2^4104 > 4p, so the
+//   * radix 2^29, N = 144 limbs (4176 bits), Montgomery R = 2^4176 > 4p, so the
 //     CIOS loop never needs a final subtraction (values stay < 2p between ops);
-//   * 27-bit limbs let every column accumulate in a 64-bit register with ONE
-//     v_mad_u64_u32 per limb product (2N products x 2^54 < 2^63 — no carry-out
-//     handling inside the loop); the gfx950 microbenchmark (profiles/r01_ubench_isa.txt)
+//     (EG_RADIX=27 keeps the first design: N = 152, R = 2^4104);
+//   * every accumulator register takes ONE v_mad_u64_u32 per limb product with no
+//     carry-out handling: a register enters its lane's top position with a 29-bit limb,
+//     takes <= 2 products per CIOS step for L = 18 steps and is split when it reaches
+//     the bottom: 36 x (2^29 + 2^6)^2 + 2^35 < 2^63.2 (squarings: 18 x (2^59 + 2^58)
+//     < 2^63.8); the gfx950 microbenchmark (profiles/r01_ubench_isa.txt)
 //     shows v_mad_u64_u32 issues at the same rate as a 32-bit add, so the cost of a
 //     Montgomery multiply is its instruction count;
 //   * one element is owned by a group of T = EG_T consecutive lanes (a DPP quad or
@@ -29,9 +32,12 @@
 
 namespace eg {
 
-constexpr int kLimbBits = 27;
+#ifndef EG_RADIX
+#define EG_RADIX 29
+#endif
+constexpr int kLimbBits = EG_RADIX;
 constexpr uint32_t kMask = (1u << kLimbBits) - 1u;
-constexpr int kN = 152;               // limbs per element
+constexpr int kN = EG_RADIX == 29 ? 144 : 152;  // limbs per element (R = 2^(kN*kLimbBits) > 4p)
 constexpr int kT = EG_T;              // lanes per element
 constexpr int kL = kN / kT;           // limbs per lane
 constexpr int kLP = (kL + 3) & ~3;    // padded limbs per lane (16-B aligned lane blocks)
@@ -40,19 +46,24 @@ constexpr int kYStride = kW + 4;      // LDS words per group slot (bank spread)
 constexpr int kWave = 64;
 constexpr int kGroupsPerWave = kWave / kT;
 static_assert(kN % kT == 0, "limbs must split evenly over the group");
+static_assert(EG_RADIX == 27 || EG_RADIX == 29, "radix 2^27 (152 limbs) or 2^29 (144 limbs)");
+static_assert(kN * kLimbBits >= 4098, "R must exceed 4p (lazy reduction: values stay < 2p)");
+// Accumulator headroom: a register lives L steps in its lane and takes <= 2 products per step
+// (x*y + m*p; with SQR one doubled x*x product + m*p).  Radix 2^29 needs L <= 18.
+static_assert(EG_RADIX == 27 || kL <= 18, "radix 2^29 overflows the 64-bit columns above 18 limbs per lane");
 static_assert(kT == 4 || kT == 8, "EG_T must be 4 or 8");
 static_assert(kW == 160, "device element format is 160 words");
 
 // Device constants of one group context (filled by the host, eg_capi.hip).
 struct MontConsts {
-  uint32_t p[kW];      // modulus limbs, device element format (radix 2^27)
+  uint32_t p[kW];      // modulus limbs, device element format (radix 2^kLimbBits)
   uint32_t r2[kW];     // R^2 mod p (normal form)        -> to-Montgomery multiplier
   uint32_t one[kW];    // R mod p (Montgomery form of 1)
   uint32_t unit[kW];   // the integer 1 (limb 0 = 1)      -> from-Montgomery multiplier
   uint32_t pw[128];    // p as 128 little-endian 32-bit words (final compare / subtract)
-  uint32_t n0;         // -p^-1 mod 2^27
-  uint32_t friendly;   // n0 == 1 (p = -1 mod 2^27): EG production group
-  uint32_t mask;       // 2^27 - 1 (read at run time so AND can fuse into DPP moves)
+  uint32_t n0;         // -p^-1 mod 2^kLimbBits
+  uint32_t friendly;   // n0 == 1 (p = -1 mod 2^kLimbBits): EG production group
+  uint32_t mask;       // 2^kLimbBits - 1 (read at run time so AND can fuse into DPP moves)
 };
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -132,33 +143,33 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t v) {
   return __builtin_amdgcn_mov_dpp(v, 0x111 /*row_shr:1*/, 0xF, 0xF, true);
 }
 
-// Montgomery multiply  x <- x * y * R^-1 mod p  (result < 2p, limbs < 2^27 + 2^11).
-//   x : this lane's L limbs (in/out), any value < 2p, limbs <= 2^27 + 2^11
+// Montgomery multiply  x <- x * y * R^-1 mod p  (result < 2p, limbs < 2^b + 2^(64-2b)+1).
+//   x : this lane's L limbs (in/out), any value < 2p, limbs <= 2^b + 2^(64-2b) + 1
 //   y : the group's LDS slot (kW words, device element format), value < 2p
 //   p : this lane's L modulus limbs (VGPRs or LDS)
-// CIOS, one radix-2^27 digit of y per step; 2L v_mad_u64_u32 + ~7 VALU per step.
+// CIOS, one radix-2^b digit of y per step; 2L v_mad_u64_u32 + ~7 VALU per step.
 //
 // SQR = true computes x^2 with y == x (the slot must hold x): the x*x part of each step
 // uses the symmetric half.  Pair {a, b} of limb indices (register indices ja, jb) is
-// added once, doubled, at the row whose register index is cyclically 1..9 behind the
-// other ((jb - ja) mod 19 in [1, 9] -> row a); pairs with ja == jb go to the smaller
-// index and the diagonal x_a^2 once.  At row i (register r = i mod 19, outer block s) every
-// lane therefore touches the SAME 10 register indices r..r+9 (mod 19): 9 doubled products
-// from 2x held in registers, and the diagonal register whose multiplier is
-// 2x_r (lanes > s), x_r (lane s) or 0 (lanes < s) -- one v_bfe_u32 with per-lane
-// (offset, width).  10 MACs + 1 VALU instead of 19 MACs per step.  All contributions
+// added once, doubled, at the row whose register index is cyclically 1..h behind the
+// other ((jb - ja) mod L in [1, h] -> row a, h = (L-1)/2); for even L the pairs at
+// distance L/2 go to the row with the smaller register index (r < L/2); pairs with
+// ja == jb go to the smaller limb index and the diagonal x_a^2 once.  At row i (register
+// r = i mod L, outer block s) every lane therefore touches the SAME register indices
+// r..r+h (mod L): doubled products from 2x held in registers, and the diagonal register
+// whose multiplier is 2x_r (lanes > s), x_r (lane s) or 0 (lanes < s) -- one v_bfe_u32
+// with per-lane (offset, width).  L = 18: 9.5 MACs + 1 VALU instead of 18.  All contributions
 // to column c still arrive by step c (each pair is added at row <= c), so the CIOS
 // quotient digits are unchanged.
 template <bool FRIENDLY, bool SQR, class PT>
 __device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
                                               const PT& p, uint32_t n0, uint32_t mask) {
-  static_assert(!SQR || kL == 19, "symmetric schedule is written for 19 limbs per lane");
   uint64_t acc[kL];
 #pragma unroll
   for (int j = 0; j < kL; ++j) acc[j] = 0;
   if constexpr (SQR) {
 #pragma unroll
-    for (int j = 0; j < kL; ++j) x[j] <<= 1;  // 2x < 2^29
+    for (int j = 0; j < kL; ++j) x[j] <<= 1;  // 2x < 2^(b+1) + 2^(65-2b) < 2^31
   }
 
 #pragma unroll 1
@@ -168,7 +179,7 @@ __device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t*
     if constexpr (SQR) {
       const int gl = glane();
       doff = (gl == s) ? 1u : 0u;   // own row: x_r = (2x_r) >> 1
-      dwid = (gl >= s) ? 30u : 0u;  // rows above: 2x_r; rows below: 0 (width 0)
+      dwid = (gl >= s) ? 31u : 0u;  // rows above: 2x_r (< 2^31); rows below: 0 (width 0)
     }
 #pragma unroll
     for (int r = 0; r < kL; ++r) {
@@ -180,8 +191,12 @@ __device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t*
           uint64_t& A = acc[(r + r) % kL];
           A = (uint64_t)d * yi + A;
         }
+        // odd L: offsets 1..(L-1)/2; even L: offsets 1..L/2-1, plus the offset-L/2 pair
+        // at the row with the smaller register index (r < L/2)
+        constexpr int kHalf = (kL - 1) / 2;
+        const int jmax = (kL % 2 == 1) ? kHalf : (r < kL / 2 ? kL / 2 : kL / 2 - 1);
 #pragma unroll
-        for (int jj = 1; jj <= (kL - 1) / 2; ++jj) {
+        for (int jj = 1; jj <= jmax; ++jj) {
           const int j = (r + jj) % kL;
           uint64_t& A = acc[(j + r) % kL];
           A = (uint64_t)x[j] * yi + A;
@@ -271,8 +286,8 @@ __device__ __forceinline__ void regs_to_lds(uint32_t* __restrict__ slot, const u
 
 // ---- conversion between 512-byte big-endian (common.proto:6-10) and limbs ----
 
-// Read bits [b, b+27) of a little-endian word array of 128 words (zero above 4096).
-__device__ __forceinline__ uint32_t bits27(const uint32_t* __restrict__ w, int b) {
+// Read bits [b, b+kLimbBits) of a little-endian word array of 128 words (zero above 4096).
+__device__ __forceinline__ uint32_t bits_limb(const uint32_t* __restrict__ w, int b) {
   const int wi = b >> 5, sh = b & 31;
   const uint32_t lo = (wi < 128) ? w[wi] : 0u;
   const uint32_t hi = (wi + 1 < 128) ? w[wi + 1] : 0u;

@@ -85,7 +85,7 @@ static void dbl_mod(Big& a, const Big& m) {
   }
   if (top || ge(a, m)) sub_in(a, m);
 }
-// words (LE, 128+) -> device element format (radix 2^27 limbs, padded lane blocks)
+// words (LE, 128+) -> device element format (radix 2^kLimbBits limbs, padded lane blocks)
 static void words_to_elem(const Big& w, uint32_t* out) {
   std::memset(out, 0, sizeof(uint32_t) * kW);
   for (int a = 0; a < kN; ++a) {
@@ -368,7 +368,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   std::memcpy(c->p_be, p_be, 512);
   std::memcpy(c->q_be, q_be, 32);
   std::memcpy(c->g_be, g_be, 512);
-  // Montgomery constants, R = 2^(27*152)
+  // Montgomery constants, R = 2^(kLimbBits*kN)
   Big P1 = p;
   P1.push_back(0);  // room for doubling
   Big r(129, 0);
@@ -383,7 +383,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   unit[0] = 1;
   words_to_elem(unit, c->h.unit);
   for (int i = 0; i < 128; ++i) c->h.pw[i] = p[i];
-  // n0 = -p^-1 mod 2^27 (Newton on 32 bits)
+  // n0 = -p^-1 mod 2^kLimbBits (Newton on 32 bits)
   uint32_t inv = 1;
   for (int i = 0; i < 6; ++i) inv *= 2u - p[0] * inv;
   c->h.n0 = (0u - inv) & kMask;

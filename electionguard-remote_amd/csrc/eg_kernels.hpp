@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) k_import(const MontConsts* __restrict_
   wave_sync();
   uint32_t x[kL];
 #pragma unroll
-  for (int j = 0; j < kL; ++j) x[j] = bits27(slot, 27 * (glane() * kL + j));
+  for (int j = 0; j < kL; ++j) x[j] = bits_limb(slot, kLimbBits * (glane() * kL + j));
   if (lt_p != nullptr && glane() == 0) {
     // lexicographic compare from the most significant word
     int cmp = 0;

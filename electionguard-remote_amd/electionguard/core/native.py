@@ -112,3 +112,11 @@ def buf(b: bytes | bytearray | memoryview):
 
 def out_buf(n: int) -> bytearray:
     return bytearray(max(n, 1))
+
+
+def version() -> str:
+    """Build string of the loaded library, e.g. 'eg_hip gfx950 radix2^29 limbs=144 ...'."""
+    lib = load()
+    b = ctypes.create_string_buffer(160)
+    check(lib, "eg_version", lib.eg_version(b, len(b)))
+    return b.value.decode()

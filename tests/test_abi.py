@@ -34,7 +34,7 @@ def test_exports_every_declared_symbol(lib):
 def test_version_and_errors_without_gpu(lib):
     buf = ctypes.create_string_buffer(128)
     assert lib.eg_version(buf, 128) == 0
-    assert b"gfx950" in buf.value and b"limbs=152" in buf.value
+    assert b"gfx950" in buf.value and b"limbs=144" in buf.value and b"radix2^29" in buf.value
     out = ctypes.c_void_p()
     even_p = bytes(511) + b"\x02"
     rc = lib.eg_ctx_create(even_p, bytes(32), bytes(512), 0, ctypes.byref(out))
