@@ -115,8 +115,14 @@ __device__ __forceinline__ uint32_t bcast_g0_and(uint32_t v, uint32_t mask) {
         : "=v"(r) : "v"(v), "v"(mask));
   }
   return r;
-#else
+#elif EG_BCAST == 1
   return bcast_g0(v) & mask;
+#else
+  // AND first on the full-mask quad_perm move (the DPP combiner folds it into
+  // v_and_b32_dpp when mask is a VGPR), then the half-row move for T = 8
+  uint32_t a = __builtin_amdgcn_mov_dpp(v, 0x00 /*quad_perm [0,0,0,0]*/, 0xF, 0xF, true) & mask;
+  if constexpr (kT == 8) a = __builtin_amdgcn_update_dpp(a, a, 0x114 /*row_shr:4*/, 0xF, 0xA, false);
+  return a;
 #endif
 }
 

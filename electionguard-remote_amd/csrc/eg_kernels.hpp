@@ -16,10 +16,10 @@ constexpr int kBlock = 256;
 #define EG_SQR 1  // squarings use the symmetric-half CIOS (eg_bignum.hpp)
 #endif
 #ifndef EG_MASK_RT
-#define EG_MASK_RT 0
+#define EG_MASK_RT 2  // 2: limb mask pinned in a VGPR so both per-step ANDs fold into v_and_b32_dpp
 #endif
 #ifndef EG_MIN_WAVES
-#define EG_MIN_WAVES 1  // __launch_bounds__ min waves per SIMD for the Montgomery kernels
+#define EG_MIN_WAVES 3  // k_pow: 3 waves/SIMD (<= 168 VGPRs; a few squaring-loop spills, measured +1.3..1.6%)
 #endif
 constexpr int kGroupsPerBlock = kBlock / kT;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -54,7 +54,10 @@ struct Mont {
     for (int j = 0; j < kL; ++j) p[j] = s[j];
 #endif
     n0 = C->n0;
-#if EG_MASK_RT
+#if EG_MASK_RT == 2
+    mask = kMask;
+    asm volatile("" : "+v"(mask));  // pin the mask in a VGPR (VOP2-DPP needs a VGPR src1)
+#elif EG_MASK_RT
     mask = C->mask;  // run-time mask: lets the DPP combiner fold AND into v_and_b32_dpp
 #else
     mask = kMask;
