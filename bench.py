@@ -49,11 +49,18 @@ def main():
     import torch
 
     dist = None
+    # EG_DIST_BACKEND=gloo rehearses the N>1 path with every rank on one GPU (host collectives)
+    backend = os.environ.get("EG_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = 0
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 

@@ -21,11 +21,19 @@ def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
+def _host_collectives(dist) -> bool:
+    """gloo (CPU tests, single-GPU rehearsals) runs the collectives on host tensors;
+    nccl (= RCCL) runs them on the device tensors over xGMI."""
+    return dist.get_backend() == "gloo"
+
+
 def all_valid(dist, ok: bool, device) -> bool:
     import torch
 
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        if _host_collectives(dist):
+            flag = flag.cpu()
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     return bool(flag.item())
 
@@ -41,8 +49,13 @@ def gather_fold_tally(dist, local_tally, fold: Callable[[np.ndarray, int, int], 
     if world == 1:
         return local_tally.cpu().numpy()
     shp = tuple(local_tally.shape)
-    gathered = torch.empty((world * shp[0],) + shp[1:], dtype=local_tally.dtype, device=local_tally.device)
-    dist.all_gather_into_tensor(gathered, local_tally.contiguous())  # rank-major concatenation
+    if _host_collectives(dist):
+        parts_l = [torch.empty(shp, dtype=local_tally.dtype) for _ in range(world)]
+        dist.all_gather(parts_l, local_tally.detach().cpu().contiguous())
+        gathered = torch.cat(parts_l, 0)
+    else:
+        gathered = torch.empty((world * shp[0],) + shp[1:], dtype=local_tally.dtype, device=local_tally.device)
+        dist.all_gather_into_tensor(gathered, local_tally.contiguous())  # rank-major concatenation
     if dist.get_rank() != dst:
         return None
     parts = gathered.cpu().numpy().reshape((world,) + shp)  # (world, n_real, 2, 512)
