@@ -131,6 +131,9 @@ def main():
     from electionguard.core import native
     radix = native.version().split("radix2^")[1].split()[0]
     total_ballots = nb * world * a.steps
+    # configs[1] = the 4x5 bench default; configs[4] = the 100-selection manifest (20 x 5)
+    cfg_name = {(4, 5): "configs[1]", (20, 5): "configs[4] shape"}.get((a.contests, a.selections), "custom manifest")
+    coll = "RCCL" if (dist is None or backend == "nccl") else backend
     value = total_ballots / el
     # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
     # 2*128^2 u32 MACs per multiply, 128*129/2 + 128^2 per squaring (group.MAC_PER_*)
@@ -150,13 +153,13 @@ def main():
         "dtype": f"u32xu32->u64 (radix-2^{radix} limbs)",
         "data": "synthetic (seeded random one-hot ballots, GPU-encrypted with random nonces)",
         "config": {
-            "workload": f"configs[1]: verify + homomorphic tally of {nb} ballots per GPU, "
+            "workload": f"{cfg_name}: verify + homomorphic tally of {nb} ballots per GPU, "
                         f"{a.contests} contests x {a.selections} selections (+1 placeholder), "
                         "EG 1.0 4096-bit production group",
             "ballots_per_gpu": nb,
             "selections_per_ballot": man.nsel,
             "fb_window_bits": a.fb_window,
-            "parallelism": f"ballot-sharded x{world}, RCCL all-gather of partial tallies",
+            "parallelism": f"ballot-sharded x{world}, {coll} all-gather of partial tallies",
         },
         "roofline": {
             "bound": "valu-int",
@@ -172,7 +175,9 @@ def main():
             "squaring_frac": round(kp.squarings / kmm, 4) if kmm else None,
         },
         "mont_ops_per_ballot": round(mm_per_ballot, 1) if mm_per_ballot else None,
-        "modexp_per_s_per_gpu": round((104 + 132) * value / world, 1),
+        # per ballot: 4 variable-base + 5 fixed-base exponentiations per selection (a0 b0 a1 b1),
+        # 2 + 3 per contest (a, b of the constant proof): 104 + 132 at 4 x (5+1)
+        "modexp_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
         "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
     }
     # HBM traffic of k_pow from the committed PMC passes of this same command

@@ -1,0 +1,766 @@
+// electionguard.hpp -- C++17 host mirror of the reference's group layer and trustee
+// plugin, above the C ABI of libeg_hip.so (include/eg_hip.h).  Header-only.
+//
+// The reference is JVM code (JDK 17 + Kotlin dependency electionguard-kotlin-
+// multiplatform-jvm:1.0-SNAPSHOT, build.gradle.kts:55); no JDK exists in this image, so
+// this is the compiled-language host side a C++ caller (or a JNI shim)
+// uses.  Names, argument meaning and error behaviour follow the reference's interfaces:
+//
+//   GroupContext / ElementModP / ElementModQ  <- KUtils.productionGroup()
+//       (src/main/java/electionguard/util/KUtils.java:10-12); elements cross the boundary
+//       as fixed-width big-endian bytes (common.proto:6-16), imported unchecked like
+//       ConvertCommonProto.importElementModP (ConvertCommonProto.java:41-57) and exported
+//       with byteArray() (ConvertCommonProto.java:111-121).
+//   DecryptingTrusteeIF                         <- RemoteDecryptingTrusteeProxy.java:30-122
+//       id() / xCoordinate() / electionPublicKey() (:33-46), directDecrypt (:48-53),
+//       compensatedDecrypt (:84-90); results in text order; a failed remote call yields an
+//       EMPTY list (:64-66, :103-105) -- GpuDecryptingTrustee throws, RemoteProxy-style
+//       callers catch and return {} (see TrusteeCallOrEmpty).
+//   Decryption::decrypt                         <- RunRemoteDecryptor.java:261-262
+//   Verifier / batchEncryption / accumulate     <- RunRemoteWorkflowTest.java:140-141,151,179-182
+//
+// Errors: a non-zero status from the C ABI throws ArithmeticException(eg_last_error()),
+// the JNI mapping INTEGRATION.md §2 describes.  Every mod-p operation runs on the GPU;
+// 256-bit mod-q scalar arithmetic (a few operations per proof / Lagrange coefficient) is
+// host arithmetic in U256 below.
+#pragma once
+
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "eg_constants.hpp"
+#include "eg_hip.h"
+
+namespace electionguard {
+
+class ArithmeticException : public std::runtime_error {
+ public:
+  explicit ArithmeticException(const std::string& what) : std::runtime_error(what) {}
+};
+
+inline void check(int rc, const char* fn) {
+  if (rc != EG_OK) throw ArithmeticException(std::string(fn) + ": " + eg_last_error());
+}
+
+// ---------------------------------------------------------------- hex helpers
+inline int hexval(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  throw std::invalid_argument("bad hex digit");
+}
+
+// big-endian hex (any length <= 2n digits, left-padded) -> n bytes
+inline void hex_to_be(const std::string& h, uint8_t* out, size_t n) {
+  if (h.size() > 2 * n) throw std::invalid_argument("hex value too wide");
+  std::memset(out, 0, n);
+  size_t off = 2 * n - h.size();
+  for (size_t i = 0; i < h.size(); ++i) {
+    const size_t d = off + i;
+    out[d / 2] |= (uint8_t)(hexval(h[i]) << ((d & 1) ? 0 : 4));
+  }
+}
+
+inline std::string be_to_hex(const uint8_t* b, size_t n) {
+  static const char* k = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (size_t i = 0; i < n; ++i) {
+    s[2 * i] = k[b[i] >> 4];
+    s[2 * i + 1] = k[b[i] & 15];
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------- U256 (mod-q scalars)
+// Little-endian 4 x 64-bit limbs.  Generic modular arithmetic for any modulus < 2^256
+// (EG q = 2^256 - 189); speed is irrelevant here (a handful of ops per proof).
+struct U256 {
+  std::array<uint64_t, 4> w{0, 0, 0, 0};
+
+  static U256 from_u64(uint64_t x) {
+    U256 r;
+    r.w[0] = x;
+    return r;
+  }
+  static U256 from_be(const uint8_t* b) {
+    U256 r;
+    for (int i = 0; i < 32; ++i) r.w[3 - i / 8] = (r.w[3 - i / 8] << 8) | b[i];
+    return r;
+  }
+  static U256 from_hex(const std::string& h) {
+    uint8_t b[32];
+    hex_to_be(h, b, 32);
+    return from_be(b);
+  }
+  void to_be(uint8_t* b) const {
+    for (int i = 0; i < 32; ++i) b[i] = (uint8_t)(w[3 - i / 8] >> (8 * (7 - i % 8)));
+  }
+  std::string hex() const {
+    uint8_t b[32];
+    to_be(b);
+    return be_to_hex(b, 32);
+  }
+  bool is_zero() const { return (w[0] | w[1] | w[2] | w[3]) == 0; }
+  bool bit(int i) const { return (w[i >> 6] >> (i & 63)) & 1; }
+  friend bool operator==(const U256& a, const U256& b) { return a.w == b.w; }
+  friend bool operator!=(const U256& a, const U256& b) { return !(a == b); }
+  friend bool operator<(const U256& a, const U256& b) {
+    for (int i = 3; i >= 0; --i)
+      if (a.w[i] != b.w[i]) return a.w[i] < b.w[i];
+    return false;
+  }
+  // a + b, returns carry
+  static uint64_t add(U256& r, const U256& a, const U256& b) {
+    unsigned __int128 c = 0;
+    for (int i = 0; i < 4; ++i) {
+      c += (unsigned __int128)a.w[i] + b.w[i];
+      r.w[i] = (uint64_t)c;
+      c >>= 64;
+    }
+    return (uint64_t)c;
+  }
+  // a - b, returns borrow
+  static uint64_t sub(U256& r, const U256& a, const U256& b) {
+    uint64_t br = 0;
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t ai = a.w[i], bi = b.w[i];
+      const uint64_t d = ai - bi - br;
+      br = (ai < bi) || (ai == bi && br) ? 1 : 0;
+      r.w[i] = d;
+    }
+    return br;
+  }
+};
+
+// Modular arithmetic over a fixed modulus m < 2^256 (values kept in [0, m)).
+struct ModQ {
+  U256 m;
+  U256 reduce_small(U256 a) const {  // a < 2^256 -> a mod m by repeated subtraction of m * 2^k
+    while (!(a < m)) {
+      U256 t = m;
+      int sh = 0;
+      while (!(t.w[3] >> 63)) {  // largest m*2^k <= a
+        U256 t2;
+        for (int i = 3; i > 0; --i) t2.w[i] = (t.w[i] << 1) | (t.w[i - 1] >> 63);
+        t2.w[0] = t.w[0] << 1;
+        if (a < t2) break;
+        t = t2;
+        ++sh;
+      }
+      U256::sub(a, a, t);
+    }
+    return a;
+  }
+  U256 add(const U256& a, const U256& b) const {
+    U256 r;
+    const uint64_t c = U256::add(r, a, b);
+    if (c || !(r < m)) U256::sub(r, r, m);
+    return r;
+  }
+  U256 sub(const U256& a, const U256& b) const {
+    U256 r;
+    if (U256::sub(r, a, b)) U256::add(r, r, m);
+    return r;
+  }
+  U256 neg(const U256& a) const { return a.is_zero() ? a : sub(m, a); }
+  U256 mul(const U256& a, const U256& b) const {
+    // 512-bit product, then bit-serial reduction r = (2r + bit) mod m from the top
+    uint64_t t[8] = {0};
+    for (int i = 0; i < 4; ++i) {
+      unsigned __int128 c = 0;
+      for (int j = 0; j < 4; ++j) {
+        c += (unsigned __int128)a.w[i] * b.w[j] + t[i + j];
+        t[i + j] = (uint64_t)c;
+        c >>= 64;
+      }
+      t[i + 4] = (uint64_t)c;
+    }
+    U256 r;
+    for (int k = 511; k >= 0; --k) {
+      const uint64_t top = r.w[3] >> 63;
+      for (int i = 3; i > 0; --i) r.w[i] = (r.w[i] << 1) | (r.w[i - 1] >> 63);
+      r.w[0] = (r.w[0] << 1) | ((t[k >> 6] >> (k & 63)) & 1);
+      if (top || !(r < m)) U256::sub(r, r, m);
+    }
+    return r;
+  }
+  U256 pow(U256 b, const U256& e) const {
+    U256 r = reduce_small(U256::from_u64(1));
+    b = reduce_small(b);
+    for (int i = 255; i >= 0; --i) {
+      r = mul(r, r);
+      if (e.bit(i)) r = mul(r, b);
+    }
+    return r;
+  }
+  U256 inv(const U256& a) const {  // m prime (q): a^(m-2)
+    if (reduce_small(a).is_zero()) throw ArithmeticException("multInv of 0 mod q");
+    U256 e;
+    U256::sub(e, m, U256::from_u64(2));
+    return pow(a, e);
+  }
+};
+
+// ---------------------------------------------------------------- elements
+class GroupContext;
+
+// ElementModP: 512-byte big-endian value (common.proto:6-10), unchecked on import.
+struct ElementModP {
+  std::array<uint8_t, EG_P_BYTES> be{};
+  const GroupContext* group = nullptr;
+
+  ElementModP() = default;
+  ElementModP(const uint8_t* b, const GroupContext* g) : group(g) { std::memcpy(be.data(), b, EG_P_BYTES); }
+  static ElementModP from_hex(const std::string& h, const GroupContext* g = nullptr) {
+    ElementModP e;
+    e.group = g;
+    hex_to_be(h, e.be.data(), EG_P_BYTES);
+    return e;
+  }
+  static ElementModP from_u64(uint64_t x, const GroupContext* g = nullptr) {
+    ElementModP e;
+    e.group = g;
+    for (int i = 0; i < 8; ++i) e.be[EG_P_BYTES - 1 - i] = (uint8_t)(x >> (8 * i));
+    return e;
+  }
+  const uint8_t* byteArray() const { return be.data(); }
+  std::string hex() const { return be_to_hex(be.data(), EG_P_BYTES); }
+  friend bool operator==(const ElementModP& a, const ElementModP& b) { return a.be == b.be; }
+  friend bool operator!=(const ElementModP& a, const ElementModP& b) { return !(a == b); }
+
+  // upstream per-element API (batches of one on the GPU)
+  inline ElementModP powP(const struct ElementModQ& e) const;
+  inline ElementModP times(const ElementModP& o) const;
+  inline ElementModP multInv() const;
+  inline ElementModP div(const ElementModP& o) const;
+};
+
+// ElementModQ: 256-bit scalar (common.proto:12-16).
+struct ElementModQ {
+  U256 v;
+  ElementModQ() = default;
+  explicit ElementModQ(const U256& x) : v(x) {}
+  static ElementModQ from_hex(const std::string& h) { return ElementModQ(U256::from_hex(h)); }
+  static ElementModQ from_be(const uint8_t* b) { return ElementModQ(U256::from_be(b)); }
+  std::array<uint8_t, EG_Q_BYTES> byteArray() const {
+    std::array<uint8_t, EG_Q_BYTES> b;
+    v.to_be(b.data());
+    return b;
+  }
+  std::string hex() const { return v.hex(); }
+  friend bool operator==(const ElementModQ& a, const ElementModQ& b) { return a.v == b.v; }
+  friend bool operator!=(const ElementModQ& a, const ElementModQ& b) { return !(a == b); }
+};
+
+struct ElGamalCiphertext {  // ConvertCommonProto.java:59-68,123-128
+  ElementModP pad, data;
+};
+struct GenericChaumPedersenProof {  // compact (c, v), common.proto:23-28
+  ElementModQ c, v;
+};
+struct DirectDecryptionAndProof {  // decrypting_trustee_rpc.proto:25-28
+  ElementModP partialDecryption;
+  GenericChaumPedersenProof proof;
+};
+struct CompensatedDecryptionAndProof {  // decrypting_trustee_rpc.proto:41-45
+  ElementModP partialDecryption;
+  GenericChaumPedersenProof proof;
+  ElementModP recoveredPublicKeyShare;
+};
+
+// ---------------------------------------------------------------- GroupContext
+class GroupContext {
+ public:
+  GroupContext(const ElementModP& p, const ElementModQ& q, const ElementModP& g, int device = 0)
+      : p_(p), g_(g), q_(q), modq_{q.v}, device_(device) {
+    const auto qb = q.byteArray();
+    check(eg_ctx_create(p.byteArray(), qb.data(), g.byteArray(), device, &ctx_), "eg_ctx_create");
+    p_.group = this;
+    g_.group = this;
+  }
+  ~GroupContext() {
+    if (ctx_) eg_ctx_destroy(ctx_);
+  }
+  GroupContext(const GroupContext&) = delete;
+  GroupContext& operator=(const GroupContext&) = delete;
+
+  // KUtils.productionGroup() (KUtils.java:10-12): the EG 1.0 4096-bit group, one per device.
+  static GroupContext& productionGroup(int device = 0) {
+    static std::mutex mu;
+    static std::map<int, std::unique_ptr<GroupContext>> groups;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& slot = groups[device];
+    if (!slot)
+      slot.reset(new GroupContext(ElementModP::from_hex(constants::kP_HEX), ElementModQ::from_hex(constants::kQ_HEX),
+                                  ElementModP::from_hex(constants::kG_HEX), device));
+    return *slot;
+  }
+
+  eg_ctx* handle() const { return ctx_; }
+  int device() const { return device_; }
+  const ElementModP& P() const { return p_; }
+  const ElementModP& G() const { return g_; }
+  const ElementModQ& Q() const { return q_; }
+  const ModQ& modq() const { return modq_; }
+
+  ElementModP binaryToElementModP(const uint8_t* b) const { return ElementModP(b, this); }
+  ElementModQ binaryToElementModQ(const uint8_t* b) const { return ElementModQ::from_be(b); }
+  ElementModQ uIntToElementModQ(uint64_t x) const { return ElementModQ(modq_.reduce_small(U256::from_u64(x))); }
+  ElementModP one() const { return ElementModP::from_u64(1, this); }
+
+  // mod-q scalar ops (ElementModQ.plus/minus/times/unaryMinus upstream)
+  ElementModQ addQ(const ElementModQ& a, const ElementModQ& b) const { return ElementModQ(modq_.add(a.v, b.v)); }
+  ElementModQ subQ(const ElementModQ& a, const ElementModQ& b) const { return ElementModQ(modq_.sub(a.v, b.v)); }
+  ElementModQ mulQ(const ElementModQ& a, const ElementModQ& b) const { return ElementModQ(modq_.mul(a.v, b.v)); }
+  ElementModQ negQ(const ElementModQ& a) const { return ElementModQ(modq_.neg(a.v)); }
+  ElementModQ invQ(const ElementModQ& a) const { return ElementModQ(modq_.inv(a.v)); }
+  ElementModQ powQ(const ElementModQ& a, const ElementModQ& e) const { return ElementModQ(modq_.pow(a.v, e.v)); }
+
+  // ---- batched group ops: the drop-in entry points ----
+  std::vector<ElementModP> powPBatch(const std::vector<ElementModP>& bases, const std::vector<ElementModQ>& exps) const {
+    if (bases.size() != exps.size()) throw std::invalid_argument("powPBatch: bases/exps length mismatch");
+    const size_t n = bases.size();
+    std::vector<uint8_t> B = packP(bases), E = packQ(exps), O(n * EG_P_BYTES);
+    if (n) check(eg_powp_batch(ctx_, B.data(), E.data(), O.data(), n), "eg_powp_batch");
+    return unpackP(O, n);
+  }
+  std::vector<ElementModP> gPowPBatch(const std::vector<ElementModQ>& exps) const {
+    const size_t n = exps.size();
+    std::vector<uint8_t> E = packQ(exps), O(n * EG_P_BYTES);
+    if (n) check(eg_fb_pow_batch(eg_ctx_g_table(ctx_), E.data(), O.data(), n), "eg_fb_pow_batch");
+    return unpackP(O, n);
+  }
+  std::vector<ElementModP> multPBatch(const std::vector<ElementModP>& a, const std::vector<ElementModP>& b) const {
+    if (a.size() != b.size()) throw std::invalid_argument("multPBatch: length mismatch");
+    const size_t n = a.size();
+    std::vector<uint8_t> A = packP(a), Bv = packP(b), O(n * EG_P_BYTES);
+    if (n) check(eg_multp_batch(ctx_, A.data(), Bv.data(), O.data(), n), "eg_multp_batch");
+    return unpackP(O, n);
+  }
+  std::vector<ElementModP> multInvBatch(const std::vector<ElementModP>& a) const {
+    const size_t n = a.size();
+    std::vector<uint8_t> A = packP(a), O(n * EG_P_BYTES);
+    if (n) check(eg_multinv_batch(ctx_, A.data(), O.data(), n), "eg_multinv_batch");
+    return unpackP(O, n);
+  }
+  // out[g] = prod_k elems[g*len + k]  (Iterable<ElementModP>.multP(), the tally)
+  std::vector<ElementModP> prodPGroups(const std::vector<ElementModP>& elems, size_t groups, size_t len) const {
+    if (elems.size() != groups * len) throw std::invalid_argument("prodPGroups: need groups*len elements");
+    std::vector<uint8_t> A = packP(elems), O(groups * EG_P_BYTES);
+    if (groups) check(eg_prod_reduce(ctx_, A.data(), groups, len, O.data()), "eg_prod_reduce");
+    return unpackP(O, groups);
+  }
+
+  // ---- per-element API (batches of one) ----
+  ElementModP gPowP(const ElementModQ& e) const { return gPowPBatch({e})[0]; }
+  ElementModP powP(const ElementModP& b, const ElementModQ& e) const { return powPBatch({b}, {e})[0]; }
+  ElementModP multP(const ElementModP& a, const ElementModP& b) const { return multPBatch({a}, {b})[0]; }
+  ElementModP multP(const std::vector<ElementModP>& xs) const {
+    return xs.empty() ? one() : prodPGroups(xs, 1, xs.size())[0];
+  }
+  ElementModP multInv(const ElementModP& a) const { return multInvBatch({a})[0]; }
+
+  // dLogG(T, maxResult) [upstream]: t with g^t = T, 0 <= t <= maxResult, else nullopt.
+  // Baby-step giant-step; every exponentiation and product on the GPU.
+  std::vector<std::optional<int64_t>> dLogGBatch(const std::vector<ElementModP>& ys, int64_t maxResult) const {
+    std::vector<std::optional<int64_t>> out(ys.size());
+    if (ys.empty() || maxResult < 0) return out;
+    int64_t m = 1;
+    while (m * m <= maxResult) ++m;
+    std::vector<ElementModQ> be(m), ge(m + 1);
+    for (int64_t j = 0; j < m; ++j) be[j] = uIntToElementModQ((uint64_t)j);
+    const ElementModQ mq = uIntToElementModQ((uint64_t)m);
+    for (int64_t i = 0; i <= m; ++i) ge[i] = negQ(mulQ(mq, uIntToElementModQ((uint64_t)i)));  // g^{-m i}
+    const auto baby = gPowPBatch(be), giants = gPowPBatch(ge);
+    std::unordered_map<std::string, int64_t> table;
+    table.reserve(2 * m);
+    for (int64_t j = 0; j < m; ++j)
+      table.emplace(std::string((const char*)baby[j].byteArray(), EG_P_BYTES), j);
+    std::vector<ElementModP> a, b;
+    a.reserve(ys.size() * (m + 1));
+    b.reserve(ys.size() * (m + 1));
+    for (const auto& y : ys)
+      for (int64_t i = 0; i <= m; ++i) {
+        a.push_back(y);
+        b.push_back(giants[i]);
+      }
+    const auto prod = multPBatch(a, b);
+    for (size_t k = 0; k < ys.size(); ++k)
+      for (int64_t i = 0; i <= m; ++i) {
+        auto it = table.find(std::string((const char*)prod[k * (m + 1) + i].byteArray(), EG_P_BYTES));
+        if (it != table.end()) {
+          const int64_t t = i * m + it->second;
+          if (t <= maxResult) out[k] = t;
+          break;
+        }
+      }
+    return out;
+  }
+  std::optional<int64_t> dLogG(const ElementModP& y, int64_t maxResult) const { return dLogGBatch({y}, maxResult)[0]; }
+
+  ElementModQ randomElementModQ(std::mt19937_64& rng, bool nonzero = true) const {
+    for (;;) {
+      U256 x;
+      for (auto& w : x.w) w = rng();
+      if (x < q_.v && (!nonzero || !x.is_zero())) return ElementModQ(x);
+    }
+  }
+
+  static std::vector<uint8_t> packP(const std::vector<ElementModP>& v) {
+    std::vector<uint8_t> out(v.size() * EG_P_BYTES);
+    for (size_t i = 0; i < v.size(); ++i) std::memcpy(&out[i * EG_P_BYTES], v[i].byteArray(), EG_P_BYTES);
+    return out;
+  }
+  static std::vector<uint8_t> packQ(const std::vector<ElementModQ>& v) {
+    std::vector<uint8_t> out(v.size() * EG_Q_BYTES);
+    for (size_t i = 0; i < v.size(); ++i) v[i].v.to_be(&out[i * EG_Q_BYTES]);
+    return out;
+  }
+  std::vector<ElementModP> unpackP(const std::vector<uint8_t>& b, size_t n) const {
+    std::vector<ElementModP> out(n);
+    for (size_t i = 0; i < n; ++i) out[i] = ElementModP(&b[i * EG_P_BYTES], this);
+    return out;
+  }
+
+ private:
+  ElementModP p_, g_;
+  ElementModQ q_;
+  ModQ modq_;
+  int device_;
+  eg_ctx* ctx_ = nullptr;
+};
+
+inline const GroupContext& group_of(const ElementModP& e) {
+  if (!e.group) throw std::logic_error("ElementModP without a GroupContext");
+  return *e.group;
+}
+inline ElementModP ElementModP::powP(const ElementModQ& e) const { return group_of(*this).powP(*this, e); }
+inline ElementModP ElementModP::times(const ElementModP& o) const { return group_of(*this).multP(*this, o); }
+inline ElementModP ElementModP::multInv() const { return group_of(*this).multInv(*this); }
+inline ElementModP ElementModP::div(const ElementModP& o) const { return times(o.multInv()); }
+
+// ---------------------------------------------------------------- key material (synthetic)
+// The reference's remote key ceremony (RunRemoteKeyCeremony.java:200-233) is out of scope;
+// this restates only its outputs: guardian i (x = i) holds P_i of degree quorum-1,
+// commitments K_ij = g^{a_ij}, and the shares P_l(x_i) of every other guardian l.
+struct GuardianKeys {
+  std::string id;
+  int x = 0;
+  std::vector<ElementModQ> coeffs;       // a_0 = secret
+  std::vector<ElementModP> commitments;  // g^{a_j}
+  std::map<std::string, ElementModQ> sharesFrom;  // l -> P_l(x)
+  const ElementModQ& secret() const { return coeffs.at(0); }
+  const ElementModP& publicKey() const { return commitments.at(0); }
+};
+
+inline ElementModQ polyEval(const GroupContext& G, const std::vector<ElementModQ>& coeffs, int x) {
+  ElementModQ acc;
+  const ElementModQ xq = G.uIntToElementModQ((uint64_t)x);
+  for (auto it = coeffs.rbegin(); it != coeffs.rend(); ++it) acc = G.addQ(G.mulQ(acc, xq), *it);
+  return acc;
+}
+
+// -> guardians and the joint key K = prod_i K_i0
+inline std::pair<std::vector<GuardianKeys>, ElementModP> keyCeremony(const GroupContext& G, int n, int quorum,
+                                                                     uint64_t seed) {
+  if (quorum < 1 || quorum > n) throw std::invalid_argument("need 1 <= quorum <= n");
+  std::mt19937_64 rng(seed);
+  std::vector<GuardianKeys> gs(n);
+  std::vector<ElementModQ> flat;
+  for (int i = 0; i < n; ++i) {
+    gs[i].id = "guardian" + std::to_string(i + 1);
+    gs[i].x = i + 1;
+    for (int j = 0; j < quorum; ++j) gs[i].coeffs.push_back(G.randomElementModQ(rng));
+    flat.insert(flat.end(), gs[i].coeffs.begin(), gs[i].coeffs.end());
+  }
+  const auto comm = G.gPowPBatch(flat);
+  std::vector<ElementModP> pk;
+  for (int i = 0; i < n; ++i) {
+    gs[i].commitments.assign(comm.begin() + (size_t)i * quorum, comm.begin() + (size_t)(i + 1) * quorum);
+    pk.push_back(gs[i].publicKey());
+  }
+  for (auto& gi : gs)
+    for (const auto& gl : gs)
+      if (gl.id != gi.id) gi.sharesFrom[gl.id] = polyEval(G, gl.coeffs, gi.x);
+  return {gs, G.multP(pk)};
+}
+
+// ---------------------------------------------------------------- trustee plugin (B2)
+class DecryptingTrusteeIF {  // RemoteDecryptingTrusteeProxy.java:30-122
+ public:
+  virtual ~DecryptingTrusteeIF() = default;
+  virtual std::string id() const = 0;
+  virtual int xCoordinate() const = 0;
+  virtual ElementModP electionPublicKey() const = 0;
+  // nonces: one per text (deterministic proofs in tests) or nullptr (random, as the
+  // reference's nonce = null, RunRemoteDecryptingTrustee.java:193)
+  virtual std::vector<DirectDecryptionAndProof> directDecrypt(const GroupContext& group,
+                                                              const std::vector<ElGamalCiphertext>& texts,
+                                                              const ElementModQ& extendedBaseHash,
+                                                              const std::vector<ElementModQ>* nonces) = 0;
+  virtual std::vector<CompensatedDecryptionAndProof> compensatedDecrypt(
+      const GroupContext& group, const std::string& missingGuardianId, const std::vector<ElGamalCiphertext>& texts,
+      const ElementModQ& extendedBaseHash, const std::vector<ElementModQ>* nonces) = 0;
+};
+
+// One GPU batch: M_i = pad_i^secret with generic CP proofs (eg_trustee_decrypt_batch).
+inline std::pair<std::vector<ElementModP>, std::vector<GenericChaumPedersenProof>> partialDecryptBatch(
+    const GroupContext& G, const ElementModQ& secret, const ElementModQ& qbar, const std::vector<ElGamalCiphertext>& texts,
+    const std::vector<ElementModQ>& nonces) {
+  const size_t n = texts.size();
+  if (nonces.size() != n) throw std::invalid_argument("one nonce per text");
+  std::vector<uint8_t> T(n * 2 * EG_P_BYTES), N = GroupContext::packQ(nonces), M(n * EG_P_BYTES), PR(n * 64);
+  for (size_t i = 0; i < n; ++i) {
+    std::memcpy(&T[(2 * i) * EG_P_BYTES], texts[i].pad.byteArray(), EG_P_BYTES);
+    std::memcpy(&T[(2 * i + 1) * EG_P_BYTES], texts[i].data.byteArray(), EG_P_BYTES);
+  }
+  const auto sb = secret.byteArray(), qb = qbar.byteArray();
+  if (n)
+    check(eg_trustee_decrypt_batch(G.handle(), sb.data(), qb.data(), T.data(), N.data(), n, M.data(), PR.data()),
+          "eg_trustee_decrypt_batch");
+  std::vector<GenericChaumPedersenProof> pr(n);
+  for (size_t i = 0; i < n; ++i) pr[i] = {ElementModQ::from_be(&PR[64 * i]), ElementModQ::from_be(&PR[64 * i + 32])};
+  return {G.unpackP(M, n), pr};
+}
+
+class GpuDecryptingTrustee : public DecryptingTrusteeIF {
+ public:
+  // commitments: every guardian's public commitments (for recovery public keys)
+  GpuDecryptingTrustee(GuardianKeys keys, std::map<std::string, std::vector<ElementModP>> commitments,
+                       uint64_t nonce_seed = std::random_device{}())
+      : keys_(std::move(keys)), commitments_(std::move(commitments)), rng_(nonce_seed) {}
+
+  std::string id() const override { return keys_.id; }
+  int xCoordinate() const override { return keys_.x; }
+  ElementModP electionPublicKey() const override { return keys_.publicKey(); }
+
+  std::vector<DirectDecryptionAndProof> directDecrypt(const GroupContext& G, const std::vector<ElGamalCiphertext>& texts,
+                                                      const ElementModQ& qbar,
+                                                      const std::vector<ElementModQ>* nonces) override {
+    const auto N = nonces ? *nonces : randomNonces(G, texts.size());
+    auto [M, pr] = partialDecryptBatch(G, keys_.secret(), qbar, texts, N);
+    std::vector<DirectDecryptionAndProof> out(texts.size());
+    for (size_t i = 0; i < texts.size(); ++i) out[i] = {M[i], pr[i]};
+    return out;
+  }
+
+  // g^{P_l(x_i)} = prod_j K_{l,j}^{x_i^j}
+  ElementModP recoveryPublicKey(const GroupContext& G, const std::string& missingId) const {
+    const auto& comm = commitments_.at(missingId);
+    std::vector<ElementModQ> e;
+    ElementModQ xj = G.uIntToElementModQ(1);
+    const ElementModQ x = G.uIntToElementModQ((uint64_t)keys_.x);
+    for (size_t j = 0; j < comm.size(); ++j) {
+      e.push_back(xj);
+      xj = G.mulQ(xj, x);
+    }
+    return G.multP(G.powPBatch(comm, e));
+  }
+
+  std::vector<CompensatedDecryptionAndProof> compensatedDecrypt(const GroupContext& G, const std::string& missingId,
+                                                                const std::vector<ElGamalCiphertext>& texts,
+                                                                const ElementModQ& qbar,
+                                                                const std::vector<ElementModQ>* nonces) override {
+    auto it = keys_.sharesFrom.find(missingId);
+    if (it == keys_.sharesFrom.end()) throw ArithmeticException("no share of " + missingId);
+    const auto N = nonces ? *nonces : randomNonces(G, texts.size());
+    auto [M, pr] = partialDecryptBatch(G, it->second, qbar, texts, N);
+    const ElementModP rk = recoveryPublicKey(G, missingId);
+    std::vector<CompensatedDecryptionAndProof> out(texts.size());
+    for (size_t i = 0; i < texts.size(); ++i) out[i] = {M[i], pr[i], rk};
+    return out;
+  }
+
+ private:
+  std::vector<ElementModQ> randomNonces(const GroupContext& G, size_t n) {
+    std::vector<ElementModQ> v(n);
+    for (auto& u : v) u = G.randomElementModQ(rng_);
+    return v;
+  }
+  GuardianKeys keys_;
+  std::map<std::string, std::vector<ElementModP>> commitments_;
+  std::mt19937_64 rng_;
+};
+
+// RemoteDecryptingTrusteeProxy behaviour: any failure -> empty list (:64-66, :103-105).
+template <class F>
+auto TrusteeCallOrEmpty(F&& f) -> decltype(f()) {
+  try {
+    return f();
+  } catch (const std::exception&) {
+    return {};
+  }
+}
+
+// Share-proof verification: a = g^v K_i^c, b = pad^v M^c, c == H(qbar, pad, data, a, b, M).
+inline std::vector<bool> verifyShares(const GroupContext& G, const ElementModQ& qbar, const std::vector<ElementModP>& Ki,
+                                      const std::vector<ElGamalCiphertext>& texts, const std::vector<ElementModP>& M,
+                                      const std::vector<GenericChaumPedersenProof>& proofs) {
+  const size_t n = texts.size();
+  if (Ki.size() != n || M.size() != n || proofs.size() != n) throw std::invalid_argument("verifyShares: sizes");
+  std::vector<uint8_t> K = GroupContext::packP(Ki), T(n * 2 * EG_P_BYTES), Mm = GroupContext::packP(M), PR(n * 64),
+                       ok(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    std::memcpy(&T[(2 * i) * EG_P_BYTES], texts[i].pad.byteArray(), EG_P_BYTES);
+    std::memcpy(&T[(2 * i + 1) * EG_P_BYTES], texts[i].data.byteArray(), EG_P_BYTES);
+    proofs[i].c.v.to_be(&PR[64 * i]);
+    proofs[i].v.v.to_be(&PR[64 * i + 32]);
+  }
+  const auto qb = qbar.byteArray();
+  if (n) check(eg_verify_shares(G.handle(), qb.data(), K.data(), T.data(), Mm.data(), PR.data(), n, ok.data()),
+               "eg_verify_shares");
+  return std::vector<bool>(ok.begin(), ok.end());
+}
+
+inline ElementModQ lagrangeCoefficient(const GroupContext& G, const std::vector<int>& xs, int xi) {
+  ElementModQ num = G.uIntToElementModQ(1), den = G.uIntToElementModQ(1);
+  for (int xj : xs)
+    if (xj != xi) {
+      num = G.mulQ(num, G.uIntToElementModQ((uint64_t)xj));
+      den = G.mulQ(den, G.subQ(G.uIntToElementModQ((uint64_t)xj), G.uIntToElementModQ((uint64_t)xi)));
+    }
+  return G.mulQ(num, G.invQ(den));
+}
+
+// Mediator combine: new Decryption(group, init, trustees, missing).decrypt(tally)
+// (RunRemoteDecryptor.java:261-262): verify every share's proof, Lagrange-weight the
+// compensated shares, M = prod M_i, T = data / M, t = dLogG(T).
+class Decryption {
+ public:
+  Decryption(const GroupContext& G, ElementModQ qbar, std::vector<DecryptingTrusteeIF*> trustees,
+             std::vector<std::string> missing)
+      : G_(G), qbar_(qbar), trustees_(std::move(trustees)), missing_(std::move(missing)) {}
+
+  std::vector<std::optional<int64_t>> decrypt(const std::vector<ElGamalCiphertext>& tally, int64_t maxCount) {
+    const size_t n = tally.size();
+    std::vector<int> xs;
+    for (auto* t : trustees_) xs.push_back(t->xCoordinate());
+    std::vector<std::vector<ElementModP>> parts;
+    for (auto* tr : trustees_) {
+      auto res = tr->directDecrypt(G_, tally, qbar_, nullptr);
+      if (res.size() != n) throw ArithmeticException("trustee " + tr->id() + " returned a short direct list");
+      std::vector<ElementModP> M;
+      std::vector<GenericChaumPedersenProof> pr;
+      for (auto& r : res) {
+        M.push_back(r.partialDecryption);
+        pr.push_back(r.proof);
+      }
+      const auto ok = verifyShares(G_, qbar_, std::vector<ElementModP>(n, tr->electionPublicKey()), tally, M, pr);
+      if (std::find(ok.begin(), ok.end(), false) != ok.end())
+        throw ArithmeticException("invalid direct decryption proof from " + tr->id());
+      parts.push_back(std::move(M));
+    }
+    for (const auto& l : missing_)
+      for (auto* tr : trustees_) {
+        auto res = tr->compensatedDecrypt(G_, l, tally, qbar_, nullptr);
+        if (res.size() != n) throw ArithmeticException("trustee " + tr->id() + " returned a short compensated list");
+        std::vector<ElementModP> M, rk;
+        std::vector<GenericChaumPedersenProof> pr;
+        for (auto& r : res) {
+          M.push_back(r.partialDecryption);
+          pr.push_back(r.proof);
+          rk.push_back(r.recoveredPublicKeyShare);
+        }
+        const auto ok = verifyShares(G_, qbar_, rk, tally, M, pr);
+        if (std::find(ok.begin(), ok.end(), false) != ok.end())
+          throw ArithmeticException("invalid compensated decryption proof from " + tr->id() + " for " + l);
+        const ElementModQ w = lagrangeCoefficient(G_, xs, tr->xCoordinate());
+        parts.push_back(G_.powPBatch(M, std::vector<ElementModQ>(n, w)));
+      }
+    const size_t k = parts.size();
+    std::vector<ElementModP> stacked;
+    stacked.reserve(n * k);
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = 0; j < k; ++j) stacked.push_back(parts[j][i]);
+    const auto M = G_.prodPGroups(stacked, n, k);
+    std::vector<ElementModP> data;
+    for (const auto& t : tally) data.push_back(t.data);
+    const auto T = G_.multPBatch(data, G_.multInvBatch(M));
+    return G_.dLogGBatch(T, maxCount);
+  }
+
+ private:
+  const GroupContext& G_;
+  ElementModQ qbar_;
+  std::vector<DecryptingTrusteeIF*> trustees_;
+  std::vector<std::string> missing_;
+};
+
+// ---------------------------------------------------------------- ballots (B1 batch users)
+struct Manifest {  // synthetic manifest shape (RandomBallotProvider, RunRemoteWorkflowTest.java:133)
+  size_t nContests = 4, nSelections = 5, votesAllowed = 1;
+  size_t spc() const { return nSelections + votesAllowed; }
+  size_t nsel() const { return nContests * spc(); }
+  size_t nReal() const { return nContests * nSelections; }
+};
+
+// Wire layout of include/eg_hip.h (big-endian, ballot-major).
+struct EncryptedBallots {
+  size_t n = 0;
+  std::vector<uint8_t> cts, rproof, cproof;  // n*nsel*2*512, n*nsel*4*32, n*nc*2*32
+};
+
+inline void setElectionKey(const GroupContext& G, const ElementModP& K, int windowBits) {
+  check(eg_set_election_key(G.handle(), K.byteArray(), windowBits), "eg_set_election_key");
+}
+
+// batchEncryption with injected nonces (RunRemoteWorkflowTest.java:140-141)
+inline EncryptedBallots batchEncryption(const GroupContext& G, const ElementModP& K, int windowBits,
+                                        const ElementModQ& qbar, const Manifest& man, size_t nb,
+                                        const std::vector<uint8_t>& votes, const std::vector<uint8_t>& selNonces,
+                                        const std::vector<uint8_t>& contestNonces) {
+  if (votes.size() != nb * man.nsel() || selNonces.size() != nb * man.nsel() * 4 * 32 ||
+      contestNonces.size() != nb * man.nContests * 32)
+    throw std::invalid_argument("batchEncryption: buffer sizes do not match the manifest");
+  EncryptedBallots eb;
+  eb.n = nb;
+  eb.cts.resize(nb * man.nsel() * 2 * EG_P_BYTES);
+  eb.rproof.resize(nb * man.nsel() * 4 * 32);
+  eb.cproof.resize(nb * man.nContests * 2 * 32);
+  setElectionKey(G, K, windowBits);
+  const auto qb = qbar.byteArray();
+  if (nb)
+    check(eg_encrypt_ballots(G.handle(), qb.data(), nb, man.nContests, man.spc(), votes.data(), selNonces.data(),
+                             contestNonces.data(), eb.cts.data(), eb.rproof.data(), eb.cproof.data()),
+          "eg_encrypt_ballots");
+  return eb;
+}
+
+// Verifier(record, 11).verify() ballot proofs + runAccumulateBallots (:151,179-182)
+struct VerifyResult {
+  std::vector<uint8_t> okSelection, okContest;
+  std::vector<ElGamalCiphertext> tally;  // n_real selections
+  bool allValid() const {
+    return std::all_of(okSelection.begin(), okSelection.end(), [](uint8_t v) { return v == 1; }) &&
+           std::all_of(okContest.begin(), okContest.end(), [](uint8_t v) { return v == 1; });
+  }
+};
+
+inline VerifyResult verifyBallots(const GroupContext& G, const ElementModP& K, const ElementModQ& qbar,
+                                  const Manifest& man, const EncryptedBallots& eb) {
+  VerifyResult r;
+  r.okSelection.assign(eb.n * man.nsel(), 0);
+  r.okContest.assign(eb.n * man.nContests, 0);
+  std::vector<uint8_t> tal(man.nReal() * 2 * EG_P_BYTES);
+  const auto qb = qbar.byteArray();
+  check(eg_verify_ballots(G.handle(), K.byteArray(), qb.data(), eb.n, man.nContests, man.spc(), man.votesAllowed,
+                          (uint32_t)man.votesAllowed, eb.cts.data(), eb.rproof.data(), eb.cproof.data(),
+                          r.okSelection.data(), r.okContest.data(), tal.data()),
+        "eg_verify_ballots");
+  for (size_t i = 0; i < man.nReal(); ++i)
+    r.tally.push_back({ElementModP(&tal[(2 * i) * EG_P_BYTES], &G), ElementModP(&tal[(2 * i + 1) * EG_P_BYTES], &G)});
+  return r;
+}
+
+}  // namespace electionguard
