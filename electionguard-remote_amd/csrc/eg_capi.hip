@@ -123,7 +123,7 @@ struct eg_fixed_base {
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_YA, W_YB, W_NSLOT
 };
 
 struct eg_ctx {
@@ -196,7 +196,10 @@ static MMCount pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
   MMCount n;
   if (S.has_base) {
     if (S.comb) {
-      n.sqr += (double)((kCombH - 1) * kCombW);
+      if (S.gather)
+        n.mul += (double)((kCombH - 1) * (S.gather - 1));  // y_k gathered from the factors' y_k
+      else
+        n.sqr += (double)((kCombH - 1) * kCombW);
       n.mul += (double)((1 << kCombH) - kCombH - 1);
     } else {
       n.mul += 14.0;
@@ -225,8 +228,12 @@ static MMCount pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
 
 
 // Run a homogeneous batch of exponentiation jobs (device job records).
+// yout (comb jobs, optional): y_1..y_4 of every job, (kCombH-1) device elements per job, kept for a
+// later gather launch; ygat: the y_k array a gather launch (S.gather > 0) multiplies together.
 static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
-                      const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1) {
+                      const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1, uint32_t* yout = nullptr,
+                      const uint32_t* ygat = nullptr) {
+  if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
   if (!njobs) return EG_OK;
   uint32_t* scr = nullptr;
   const size_t per = S.has_base ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
@@ -244,7 +251,8 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
       HIPCHK(hipEventRecord(pr.a, c->stream));
     }
     LAUNCH_F(c, k_pow, dim3(grid_for(nj)), c->d, S, d_jobs + off * kJobWords,
-                       (uint32_t)nj, d_elems, d_scal, d_out, scr, f0, f1);
+                       (uint32_t)nj, d_elems, d_scal, d_out, scr, f0, f1,
+                       yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat);
     HIPCHK(hipGetLastError());
     if (c->timing) {
       HIPCHK(hipEventRecord(pr.b, c->stream));

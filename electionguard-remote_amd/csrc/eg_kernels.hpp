@@ -241,6 +241,9 @@ struct PowShape {
   uint32_t has_base, nout, nfb[2], tab[2][2];
   uint32_t exp_bytes;  // variable-base exponent length (32, or 512 for inverses)
   uint32_t comb;       // 1: Lim-Lee comb (h = 5) shared by the job's exponents (32-byte only)
+  uint32_t gather;     // comb jobs whose base is a PRODUCT of `gather` earlier comb bases (the contest
+                       // aggregates A = prod alpha, B = prod beta): y_k = prod of their y_k (ygat,
+                       // job J[2] onwards) instead of 208 squarings; 0 = none
 };
 
 // Lim-Lee comb parameters for 256-bit exponents: 5 rows of 52 bits.
@@ -281,7 +284,8 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
                                                 const uint32_t* __restrict__ elems,
                                                 const uint8_t* __restrict__ scalars,
                                                 uint32_t* __restrict__ out, uint32_t* __restrict__ scratch,
-                                                FbTab fb0, FbTab fb1) {
+                                                FbTab fb0, FbTab fb1, uint32_t* __restrict__ yout,
+                                                const uint32_t* __restrict__ ygat) {
   __shared__ uint8_t s_dig[kGroupsPerBlock][64];
   const uint32_t gid = group_id();
   const uint32_t jb = gid < njobs ? gid : njobs - 1;
@@ -302,8 +306,11 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   // of one ~150-VGPR body instead of several).  All branches are launch-uniform.
   //   window path: table B^0..B^15 (14 MM), per exponent 63 x (4 sq + 1 mul)
   //   comb path  : y_k = B^(2^(52k)) (208 sq), table of the 32 subset products (26 MM),
-  //                per exponent 51 x (1 sq + 1 mul) from column digits
-  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3, kPre = 4, kCTab = 5, kComb = 6 };
+  //                per exponent 51 x (1 sq + 1 mul) from column digits; yout (if set) keeps
+  //                y_1..y_4 of every job for a later gather launch
+  //   gather     : B = prod of S.gather comb bases whose y_k are in ygat (jobs J[2] ..):
+  //                y_k = prod of theirs, 4 x (gather-1) MM instead of 208 squarings
+  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3, kPre = 4, kCTab = 5, kComb = 6, kGather = 7 };
   int phase = kBegin, k = 2, w = 0, sub = 0;
   uint32_t o = 0, t = 0, kf = 0;
   bool x_is_one = true;
@@ -316,6 +323,12 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     store_elem(tbl + kW, x);
     phase = comb ? kPre : kTable;
     k = comb ? 0 : 2;
+    if (comb && S.gather) {
+      phase = kGather;
+      k = 1;
+      sub = 1;
+      load_elem(x, ygat + ((size_t)J[2] * (kCombH - 1)) * kW);
+    }
   }
   while (true) {
     const uint32_t* ysrc = nullptr;  // nullptr: square
@@ -326,6 +339,17 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         phase = kCTab;
         k = 3;
         continue;
+      }
+      if (phase == kGather) {  // y_k = prod_i y_k(base i), i = J[2] .. J[2] + gather - 1
+        if (sub >= (int)S.gather) {
+          store_elem(tbl + ((size_t)1 << k) * kW, x);
+          sub = 1;
+          if (++k > kCombH - 1) { phase = kCTab; k = 3; continue; }
+          load_elem(x, ygat + ((size_t)J[2] * (kCombH - 1) + (k - 1)) * kW);
+          continue;
+        }
+        ysrc = ygat + ((size_t)(J[2] + sub) * (kCombH - 1) + (k - 1)) * kW;
+        break;
       }
       if (phase == kCTab) {  // entry k = (k & (k-1)) * (lowest bit of k)
         while (k < (1 << kCombH) && (k & (k - 1)) == 0) ++k;
@@ -419,8 +443,12 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     else if (phase == kVar) { if (++sub == 5) { sub = 0; ++w; } }
     else if (phase == kPre) {
       ++k;
-      if (k % kCombW == 0) store_elem(tbl + ((size_t)1 << (k / kCombW)) * kW, x);
+      if (k % kCombW == 0) {
+        store_elem(tbl + ((size_t)1 << (k / kCombW)) * kW, x);
+        if (yout != nullptr && gid < njobs) store_elem(yout + ((size_t)gid * (kCombH - 1) + (k / kCombW - 1)) * kW, x);
+      }
     }
+    else if (phase == kGather) { ++sub; }
     else if (phase == kCTab) { store_elem(tbl + (size_t)k * kW, x); ++k; }
     else if (phase == kComb) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
     else { ++kf; }
