@@ -130,6 +130,8 @@ def main():
 
     from electionguard.core import native
     radix = native.version().split("radix2^")[1].split()[0]
+    import hashlib
+    build_id = hashlib.md5(Path(native.lib_path()).read_bytes()).hexdigest()[:12]
     total_ballots = nb * world * a.steps
     # configs[1] = the 4x5 bench default; configs[4] = the 100-selection manifest (20 x 5)
     cfg_name = {(4, 5): "configs[1]", (20, 5): "configs[4] shape"}.get((a.contests, a.selections), "custom manifest")
@@ -179,14 +181,16 @@ def main():
         # 2 + 3 per contest (a, b of the constant proof): 104 + 132 at 4 x (5+1)
         "modexp_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
         "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
+        "build": build_id,
     }
     # HBM traffic of k_pow from the committed PMC passes of this same command
-    # (tools/profile_round.sh); only quoted when the profiled workload matches this run's.
+    # (tools/profile_round.sh); only quoted when the profiled workload AND the library build
+    # (md5 of libeg_hip.so) match this run's.
     prof = ROOT / "profiles" / "r01_pmc_kpow.json"
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
-            if pm.get("bench_config") == out["config"]:
+            if pm.get("bench_config") == out["config"] and pm.get("bench_build") == build_id:
                 out["roofline"]["traffic"] = round(pm["traffic"]["hbm_bytes_per_launch"])
                 out["roofline"]["traffic_source"] = "profiles/r01_pmc_kpow.json"
         except (KeyError, ValueError, TypeError):

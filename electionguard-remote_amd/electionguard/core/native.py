@@ -120,3 +120,8 @@ def version() -> str:
     b = ctypes.create_string_buffer(160)
     check(lib, "eg_version", lib.eg_version(b, len(b)))
     return b.value.decode()
+
+
+def lib_path() -> Path:
+    """Path of the library load() uses (EG_LIB override or the in-tree build)."""
+    return Path(os.environ["EG_LIB"]) if os.environ.get("EG_LIB") else LIB_PATH

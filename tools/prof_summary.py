@@ -84,6 +84,7 @@ def main():
                   "timed region = last `launches` k_pow dispatches; FETCH_SIZE x2 (gfx950)",
         "bench": {k: bl[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup")},
         "bench_config": bl["config"],
+        "bench_build": bl.get("build"),
         "bench_roofline": bl["roofline"],
         "rocprof": {
             "kpow_dispatches_all": len(durs),
