@@ -230,35 +230,62 @@ static MMCount pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
 // Run a homogeneous batch of exponentiation jobs (device job records).
 // yout (comb jobs, optional): y_1..y_4 of every job, (kCombH-1) device elements per job, kept for a
 // later gather launch; ygat: the y_k array a gather launch (S.gather > 0) multiplies together.
+// tail (optional): a second, independent job population (shape tail->S) appended to the LAST
+// sub-launch so its short jobs fill that launch's tail (PowPart in eg_kernels.hpp).
+struct PowTail {
+  PowShape S;
+  const uint32_t* jobs;
+  size_t njobs;
+  uint32_t* yout;
+  const uint32_t* ygat;
+};
+static size_t pow_scratch_per_group(const PowShape& S) {
+  return S.has_base ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
+}
 static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
                       const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1, uint32_t* yout = nullptr,
-                      const uint32_t* ygat = nullptr) {
+                      const uint32_t* ygat = nullptr, const PowTail* tail = nullptr) {
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
-  if (!njobs) return EG_OK;
-  uint32_t* scr = nullptr;
-  const size_t per = S.has_base ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
-  // bound the per-launch scratch (table of 16 powers per job)
+  if (tail && tail->S.gather && (!tail->S.comb || !tail->ygat))
+    return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
+  if (tail && !tail->njobs) tail = nullptr;
+  if (!njobs && !tail) return EG_OK;
+  const size_t per = pow_scratch_per_group(S);
+  const size_t per1 = tail ? pow_scratch_per_group(tail->S) : 0;
+  // bound the per-launch scratch (table of 16/32 powers per job)
   const size_t max_jobs = (size_t)1 << 18;
   const MMCount mm_job = pow_job_mm(S, f0, f1);
-  for (size_t off = 0; off < njobs; off += max_jobs) {
+  const MMCount mm_tail = tail ? pow_job_mm(tail->S, f0, f1) : MMCount{};
+  size_t off = 0;
+  do {
     const size_t nj = std::min(max_jobs, njobs - off);
-    int rc = ws_get(c, W_SCR, padded_groups(nj) * per, (void**)&scr);
+    const bool last = off + nj >= njobs;
+    const size_t nt = (last && tail) ? tail->njobs : 0;
+    uint32_t* scr = nullptr;
+    int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
     if (rc) return rc;
-    ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj, mm_job.sqr * (double)nj};
+    PowPart P0{S, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
+               yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat};
+    PowPart P1{};
+    if (nt) {
+      P1 = PowPart{tail->S, tail->jobs, (uint32_t)nt, grid_for(nt),
+                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat};
+    }
+    ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
+               mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
     if (c->timing) {
       HIPCHK(hipEventCreate(&pr.a));
       HIPCHK(hipEventCreate(&pr.b));
       HIPCHK(hipEventRecord(pr.a, c->stream));
     }
-    LAUNCH_F(c, k_pow, dim3(grid_for(nj)), c->d, S, d_jobs + off * kJobWords,
-                       (uint32_t)nj, d_elems, d_scal, d_out, scr, f0, f1,
-                       yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat);
+    LAUNCH_F(c, k_pow, dim3(P0.nblocks + P1.nblocks), c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
     HIPCHK(hipGetLastError());
     if (c->timing) {
       HIPCHK(hipEventRecord(pr.b, c->stream));
       prof_of(c).push_back(pr);
     }
-  }
+    off += nj;
+  } while (off < njobs);
   return EG_OK;
 }
 

@@ -278,16 +278,35 @@ __device__ __forceinline__ void fb_ladder(const Mont<F>& M, uint32_t (&x)[kL], u
   }
 }
 
+// One launch may carry two job populations of different shapes (e.g. the beta jobs and the
+// contest-A jobs that only depend on the previous launch): part 0 owns the first P0.nblocks
+// workgroups, part 1 the rest, so the short part-1 jobs fill the tail of part 0 instead of
+// running as a separate, under-filled launch.  The shape stays workgroup-uniform.
+struct PowPart {
+  PowShape S;
+  const uint32_t* jobs;
+  uint32_t njobs;
+  uint32_t nblocks;   // workgroups of this part
+  uint32_t* scratch;  // per-group table (comb: 32 elements, window: 16)
+  uint32_t* yout;     // comb y_1..y_4 per job (optional)
+  const uint32_t* ygat;  // gather source (S.gather > 0)
+};
+
 template <bool F>
-__global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowShape S,
-                                                const uint32_t* __restrict__ jobs, uint32_t njobs,
-                                                const uint32_t* __restrict__ elems,
+__global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowPart P0,
+                                                PowPart P1, const uint32_t* __restrict__ elems,
                                                 const uint8_t* __restrict__ scalars,
-                                                uint32_t* __restrict__ out, uint32_t* __restrict__ scratch,
-                                                FbTab fb0, FbTab fb1, uint32_t* __restrict__ yout,
-                                                const uint32_t* __restrict__ ygat) {
+                                                uint32_t* __restrict__ out, FbTab fb0, FbTab fb1) {
   __shared__ uint8_t s_dig[kGroupsPerBlock][64];
-  const uint32_t gid = group_id();
+  const bool second = blockIdx.x >= P0.nblocks;
+  const PowPart& P = second ? P1 : P0;  // kernarg memory: shape fields stay scalar loads
+  const PowShape& S = P.S;
+  const uint32_t* __restrict__ jobs = P.jobs;
+  const uint32_t njobs = P.njobs;
+  uint32_t* __restrict__ scratch = P.scratch;
+  uint32_t* __restrict__ yout = P.yout;
+  const uint32_t* __restrict__ ygat = P.ygat;
+  const uint32_t gid = (blockIdx.x - (second ? P0.nblocks : 0u)) * kGroupsPerBlock + threadIdx.x / kT;
   const uint32_t jb = gid < njobs ? gid : njobs - 1;
   const uint32_t* J = jobs + (size_t)jb * kJobWords;
   uint32_t* slot = group_slot();
