@@ -1,0 +1,81 @@
+"""GPU: the launch-splitting paths of the fused verifier (eg_capi_ballot.inc / launch_pow).
+
+* > 2^18 selection jobs in one chunk: k_pow is split into sub-launches and the gathered
+  contest-A jobs ride in the LAST sub-launch of the beta jobs (PowPart tail);
+* > 16384 ballots: two verify chunks, the running tally is combined across chunks.
+Both must give every verdict valid and a tally equal to the product of all ballots'
+ciphertexts (checked against the independent C oracle / CPython products); a tampered
+proof in the second sub-launch / second chunk must be flagged exactly.
+"""
+import numpy as np
+import pytest
+
+import eg_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _encrypt(group, man, nb, seed):
+    from electionguard.ballot import ElectionKey, batch_encryption, random_scalars, random_votes
+    from electionguard.keyceremony import key_ceremony
+    gk, K = key_ceremony(group, 3, 3, seed=seed)
+    key = ElectionKey(group, K, window_bits=12)
+    rng = np.random.default_rng(seed)
+    votes = random_votes(rng, man, nb)
+    qbar = 777 + seed
+    eb = batch_encryption(group, key, qbar, man, votes, random_scalars(rng, (nb, man.nsel, 4), group.q),
+                          random_scalars(rng, (nb, man.n_contests), group.q))
+    return key, K, qbar, eb
+
+
+def _tally_products(man, eb):
+    p = O.production_group().p
+    out = np.zeros((man.n_real, 2, 512), np.uint8)
+    for s in range(man.n_real):
+        k, r = divmod(s, man.n_selections)
+        i = k * man.spc + r
+        for c in range(2):
+            acc = 1
+            col = eb.cts[:, i, c]
+            for b in range(eb.n):
+                acc = acc * int.from_bytes(col[b].tobytes(), "big") % p
+            out[s, c] = np.frombuffer(acc.to_bytes(512, "big"), np.uint8)
+    return out
+
+
+def test_split_sublaunches_with_contest_tail(group):
+    from electionguard.ballot import EncryptedBallots, Manifest, Verifier
+    man = Manifest(4, 5, 1)
+    nb = 11000  # 264,000 selection jobs > 2^18 -> two k_pow sub-launches per job type
+    key, K, qbar, eb = _encrypt(group, man, nb, 31)
+    V = Verifier(group, key, qbar, man)
+    ok_s, ok_c, tally = V.verify(eb)
+    assert ok_s.all() and ok_c.all()
+    assert np.array_equal(tally, _tally_products(man, eb))
+    # tamper: a selection proof in the second sub-launch and a contest proof near the end
+    rp, cp = eb.rproof.copy(), eb.cproof.copy()
+    rp[10990, 3, 1, 0] ^= 0x80   # job 10990*24+3 = 263,763 > 2^18
+    cp[10500, 2, 0, 31] ^= 0x01
+    ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, cp), with_tally=False)
+    assert np.argwhere(~ok_s).tolist() == [[10990, 3]]
+    assert np.argwhere(~ok_c).tolist() == [[10500, 2]]
+
+
+def test_two_chunks_tally_combined(group):
+    from electionguard.ballot import EncryptedBallots, Manifest, Verifier
+    man = Manifest(1, 2, 1)
+    nb = 16384 + 700  # two verify chunks (CH = 16384 ballots)
+    key, K, qbar, eb = _encrypt(group, man, nb, 47)
+    V = Verifier(group, key, qbar, man)
+    ok_s, ok_c, tally = V.verify(eb)
+    assert ok_s.all() and ok_c.all()
+    assert np.array_equal(tally, _tally_products(man, eb))
+    # linearity across the chunk boundary
+    _, _, t1 = V.verify(eb.slice(0, 16384))
+    _, _, t2 = V.verify(eb.slice(16384, nb))
+    prod = group.multP_batch(t1.reshape(-1, 512), t2.reshape(-1, 512)).reshape(tally.shape)
+    assert np.array_equal(prod, tally)
+    rp = eb.rproof.copy()
+    rp[17000, 1, 3, 5] ^= 0x02
+    ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, eb.cproof), with_tally=False)
+    assert np.argwhere(~ok_s).tolist() == [[17000, 1]] and ok_c.all()
