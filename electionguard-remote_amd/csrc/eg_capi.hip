@@ -430,16 +430,20 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     delete c;
     return fail(EG_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
-  HIPCHK(hipMalloc(&c->d, sizeof(MontConsts)));
-  HIPCHK(hipMemcpy(c->d, &c->h, sizeof(MontConsts), hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&c->d_q, 32));
-  HIPCHK(hipMemcpy(c->d_q, q_be, 32, hipMemcpyHostToDevice));
-  HIPCHK(hipMalloc(&c->d_qbar, 32));
-  std::lock_guard<std::mutex> lk(c->mu);
-  int rc = fb_create_locked(c, g_be, 8, &c->gtab);
-  if (rc) {
-    delete c;
-    return rc;
+  auto setup = [&]() -> int {
+    HIPCHK(hipMalloc(&c->d, sizeof(MontConsts)));
+    HIPCHK(hipMemcpy(c->d, &c->h, sizeof(MontConsts), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&c->d_q, 32));
+    HIPCHK(hipMemcpy(c->d_q, q_be, 32, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&c->d_qbar, 32));
+    std::lock_guard<std::mutex> lk(c->mu);
+    return fb_create_locked(c, g_be, 8, &c->gtab);
+  };
+  const int rc = setup();
+  if (rc) {  // the ctx lock is released here; free whatever was allocated, keep the message
+    const std::string msg = g_err;
+    eg_ctx_destroy(c);
+    return fail(rc, msg);
   }
   *out = c;
   return EG_OK;
