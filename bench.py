@@ -180,6 +180,8 @@ def main():
         # per ballot: 4 variable-base + 5 fixed-base exponentiations per selection (a0 b0 a1 b1),
         # 2 + 3 per contest (a, b of the constant proof): 104 + 132 at 4 x (5+1)
         "modexp_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
+        "modexp_var_base_per_s_per_gpu": round((4 * man.nsel + 2 * man.n_contests) * value / world, 1),
+        "modexp_fixed_base_per_s_per_gpu": round((5 * man.nsel + 3 * man.n_contests) * value / world, 1),
         "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
         "build": build_id,
     }
