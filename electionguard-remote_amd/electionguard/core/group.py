@@ -306,12 +306,15 @@ class ElementModQ:
 
 
 _PRODUCTION: dict = {}
+_PRODUCTION_LOCK = threading.Lock()
 
 
 def productionGroup(device: int = 0) -> GroupContext:
-    """``KUtils.productionGroup()`` (KUtils.java:10-12): the EG 1.0 4096-bit group."""
-    g = _PRODUCTION.get(device)
-    if g is None:
-        g = GroupContext(_P, _Q, _G, device=device)
-        _PRODUCTION[device] = g
-    return g
+    """``KUtils.productionGroup()`` (KUtils.java:10-12): the EG 1.0 4096-bit group, one
+    context per device even when first requested from several threads at once."""
+    with _PRODUCTION_LOCK:
+        g = _PRODUCTION.get(device)
+        if g is None:
+            g = GroupContext(_P, _Q, _G, device=device)
+            _PRODUCTION[device] = g
+        return g
