@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <map>
 #include <mutex>
 #include <string>
@@ -143,6 +144,9 @@ struct eg_ctx {
   uint8_t K_be[512];
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
+  // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
+  // most recently used first
+  std::vector<std::pair<std::array<uint8_t, 512>, eg_fixed_base*>> share_keys;
 };
 static std::vector<ProfRec>& prof_of(eg_ctx* c) { return c->prof; }
 
@@ -462,6 +466,7 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
   hipStreamSynchronize(c->stream);
   eg_fixed_base_destroy(c->gtab);
   eg_fixed_base_destroy(c->Ktab);
+  for (auto& kv : c->share_keys) eg_fixed_base_destroy(kv.second);
   for (auto& b : c->ws)
     if (b.ptr) hipFree(b.ptr);
   for (auto& kv : c->cache)

@@ -74,3 +74,40 @@ def test_verify_shares_rejects_bad_proof(group):
     proofs[1] = GenericChaumPedersenProof(proofs[1].c, (proofs[1].v + 1) % og.q)
     ok = verify_shares(group, qbar, [gs[0].K] * 3, [(t.pad, t.data) for t in texts], [m for m, _ in res], proofs)
     assert list(ok) == [True, False, True]
+
+
+def test_verify_shares_large_batch_key_table(group):
+    """>= 8192 shares of one trustee: eg_verify_shares switches a = g^v K_i^c to a cached
+    fixed-base table of K_i; every honest proof verifies, tampered ones (c or v) fail, and a
+    batch mixing two keys takes the window path with the same verdicts."""
+    import ctypes
+    from electionguard.ballot import random_scalars
+    from electionguard.core import native
+    from electionguard.core.group import p_bytes, q_bytes
+    from electionguard.decrypt import partial_decrypt_batch
+    from electionguard.keyceremony import key_ceremony
+    gk, K = key_ceremony(group, 2, 2, seed=77)
+    rng = np.random.default_rng(77)
+    n = 8200
+    R = random_scalars(rng, (n,), group.q)
+    T = np.ascontiguousarray(np.stack([group.gPowP_batch(R), group.powP_batch([K] * n, R)], axis=1))
+    qbar = 0xABCDEF
+    M, pr = partial_decrypt_batch(group, gk[0].secret, qbar, T, random_scalars(rng, (n,), group.q))
+    pr = pr.copy()
+    pr[17, 1, 31] ^= 1      # v
+    pr[8199, 0, 0] ^= 0x40  # c
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+
+    def verify(keys):
+        ok = np.zeros(n, np.uint8)
+        native.check(group._lib, "eg_verify_shares",
+                     group._lib.eg_verify_shares(group.handle, native.buf(q_bytes(qbar)), ptr(keys), ptr(T), ptr(M),
+                                                 ptr(pr), n, ptr(ok)))
+        return np.argwhere(ok == 0).reshape(-1).tolist()
+
+    Ki = np.ascontiguousarray(np.tile(np.frombuffer(p_bytes(gk[0].public_key), np.uint8), (n, 1)))
+    assert verify(Ki) == [17, 8199]   # table path
+    assert verify(Ki) == [17, 8199]   # cached table
+    mixed = Ki.copy()
+    mixed[5] = np.frombuffer(p_bytes(gk[1].public_key), np.uint8)  # wrong key for share 5 -> window path
+    assert verify(mixed) == [5, 17, 8199]
