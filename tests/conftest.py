@@ -22,6 +22,12 @@ def oracle_group():
 
 @pytest.fixture(scope="session")
 def group():
+    # torch bundles its own libamdhip64.so.7: it must bring up its HIP runtime BEFORE
+    # libeg_hip.so pulls in the system one, or torch sees no GPU (tests that hand torch
+    # device tensors to the C ABI need both).  bench.py has the same order.
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from electionguard.core import productionGroup
     return productionGroup(0)
 
