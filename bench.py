@@ -25,6 +25,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "electionguard-remote_amd"))
 
 PEAK_TMAC = 256 * 64 * 2.4e9 / 1e12   # 256 CUs x 64 v_mad_u64_u32 lanes/clk/CU x 2.4 GHz (profiles/r01_ubench_isa.txt)
+# measured v_mad_u64_u32 issue ceiling at 3 waves/SIMD (k_pow's occupancy): 58.4 lane-MAC/clk/CU,
+# 4.4 cycles per wave-instruction (profiles/r01_ubench_banks.txt)
+ISSUE_TMAC = 256 * 58.4 * 2.4e9 / 1e12
 
 
 def parse():
@@ -170,6 +173,8 @@ def main():
             "peak": round(PEAK_TMAC, 2),
             "unit": "TMAC/s (u32xu32+u64 v_mad_u64_u32)",
             "frac": round(achieved / PEAK_TMAC, 4) if achieved else None,
+            "measured_issue_peak": round(ISSUE_TMAC, 2),
+            "frac_of_measured_issue_peak": round(achieved / ISSUE_TMAC, 4) if achieved else None,
             "traffic": None,
             "kernel_ms_per_launch": round(kms / max(klaunch, 1), 3),
             "launches": klaunch,
