@@ -29,7 +29,7 @@ import numpy as np
 
 from .core import native
 from .core.group import GroupContext, as_p_array, p_bytes, q_bytes
-from .keyceremony import GuardianKeys, poly_eval
+from .keyceremony import GuardianKeys, backup_label, backup_open, poly_eval
 
 
 @dataclass
@@ -101,6 +101,7 @@ class DecryptingTrustee:
         self.group = group
         self.keys = keys
         self.commitments = commitments  # every guardian's public commitments (for recovery keys)
+        self._shares: Dict[str, int] = {}  # decrypted backups, by missing guardian id
 
     def id(self) -> str:
         return self.keys.gid
@@ -126,11 +127,29 @@ class DecryptingTrustee:
         pw = self.group.powP_batch(comm, exps)
         return _be_int(self.group.prodP_groups(pw, 1, len(comm))[0])
 
+    def share_of(self, missing_id: str) -> int:
+        """P_l(x_i): decrypt guardian l's key-ceremony backup with this trustee's secret
+        (k = c0^{s_i} on the GPU, then the KDF / MAC of keyceremony.backup_open); callers that
+        only hold decrypted shares fall back to ``shares_from``."""
+        cached = self._shares.get(missing_id)
+        if cached is not None:
+            return cached
+        if missing_id in self.keys.backups_from:
+            c0, c1, c2 = self.keys.backups_from[missing_id]
+            k = _be_int(self.group.powP_batch([c0], [self.keys.secret])[0])
+            share = backup_open(c0, k, c1, c2, backup_label(missing_id, self.keys.gid))
+            if share is None:
+                raise ValueError(f"share backup from {missing_id} fails its MAC")
+        elif missing_id in self.keys.shares_from:
+            share = self.keys.shares_from[missing_id]
+        else:
+            raise KeyError(f"no share of {missing_id}")
+        self._shares[missing_id] = share
+        return share
+
     def compensatedDecrypt(self, group: GroupContext, missingGuardianId: str, texts, extendedBaseHash: int,
                            nonce: Optional[Sequence[int]] = None) -> List[CompensatedDecryptionAndProof]:
-        if missingGuardianId not in self.keys.shares_from:
-            raise KeyError(f"no share of {missingGuardianId}")
-        share = self.keys.shares_from[missingGuardianId]
+        share = self.share_of(missingGuardianId)
         T = _texts_array(texts)
         M, pr = partial_decrypt_batch(group, share, extendedBaseHash, T, _nonces(group, len(T), nonce))
         rk = self.recovery_public_key(missingGuardianId)

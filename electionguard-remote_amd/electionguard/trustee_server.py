@@ -20,7 +20,8 @@ def load_trustee_file(path):
 
     d = json.loads(open(path).read())
     g = GuardianKeys(d["id"], d["x"], [int(a, 16) for a in d["coeffs"]], [int(k, 16) for k in d["commitments"]],
-                     {k: int(v, 16) for k, v in d["shares_from"].items()})
+                     {}, {k: (int(v[0], 16), bytes.fromhex(v[1]), bytes.fromhex(v[2]))
+                          for k, v in d["backups_from"].items()})
     comm = {k: [int(x, 16) for x in v] for k, v in d["all_commitments"].items()}
     return g, comm
 
@@ -28,7 +29,8 @@ def load_trustee_file(path):
 def write_trustee_file(path, g, all_commitments):
     json.dump({"id": g.gid, "x": g.x, "coeffs": [hex(a) for a in g.coeffs],
                "commitments": [hex(k) for k in g.commitments],
-               "shares_from": {k: hex(v) for k, v in g.shares_from.items()},
+               # the other guardians' shares travel only as their encrypted backups
+               "backups_from": {k: [hex(c0), c1.hex(), c2.hex()] for k, (c0, c1, c2) in g.backups_from.items()},
                "all_commitments": {k: [hex(x) for x in v] for k, v in all_commitments.items()}},
               open(path, "w"))
 

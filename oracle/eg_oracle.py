@@ -360,6 +360,47 @@ def key_ceremony(G: Group, n: int, quorum: int, rng: random.Random) -> Tuple[Lis
     return gs, K
 
 
+# --------------------------------------------------------------------------------------
+# Key-ceremony share backups (HashedElGamalCiphertext) — SURVEY §8a row a12: a trustee's
+# compensatedDecrypt first decrypts guardian l's backup of P_l(x_i) with its own secret
+# (1 variable-base powP + SHA/HMAC), RunRemoteDecryptingTrustee.java:227-232 via upstream.
+# The upstream KDF / MAC layout is not in the container (unpinned); this restatement
+# defines it and the GPU-backed trustee must match it:
+#   c0 = g^r,  k = K_i^r = c0^{s_i}  (512 B BE),  kk = SHA256(c0 || k)
+#   stream = HMAC-SHA256(kk, 0x01 || "share" || l || i),  mac_key = HMAC-SHA256(kk, 0x02 || ...)
+#   c1 = P_l(x_i) (32 B BE) XOR stream,  c2 = HMAC-SHA256(mac_key, c0 || c1)
+# --------------------------------------------------------------------------------------
+
+def _backup_keys(c0: int, k: int, label: bytes) -> Tuple[bytes, bytes]:
+    import hmac
+    kk = hashlib.sha256(c0.to_bytes(512, "big") + k.to_bytes(512, "big")).digest()
+    stream = hmac.new(kk, b"\x01share" + label, hashlib.sha256).digest()
+    mac_key = hmac.new(kk, b"\x02share" + label, hashlib.sha256).digest()
+    return stream, mac_key
+
+
+def backup_label(from_gid: str, to_gid: str) -> bytes:
+    return from_gid.encode() + b"|" + to_gid.encode()
+
+
+def backup_encrypt(G: Group, K_to: int, share: int, r: int, label: bytes) -> Tuple[int, bytes, bytes]:
+    import hmac
+    c0 = G.gPowP(r)
+    stream, mac_key = _backup_keys(c0, G.powP(K_to, r), label)
+    c1 = bytes(a ^ b for a, b in zip(share.to_bytes(32, "big"), stream))
+    return c0, c1, hmac.new(mac_key, c0.to_bytes(512, "big") + c1, hashlib.sha256).digest()
+
+
+def backup_decrypt(G: Group, s_to: int, backup: Tuple[int, bytes, bytes], label: bytes) -> Optional[int]:
+    """-> P_l(x_i), or None when the MAC does not verify."""
+    import hmac
+    c0, c1, c2 = backup
+    stream, mac_key = _backup_keys(c0, G.powP(c0, s_to), label)
+    if not hmac.compare_digest(c2, hmac.new(mac_key, c0.to_bytes(512, "big") + c1, hashlib.sha256).digest()):
+        return None
+    return int.from_bytes(bytes(a ^ b for a, b in zip(c1, stream)), "big")
+
+
 def direct_decrypt(G: Group, qbar: int, gd: Guardian, texts: Sequence[Ciphertext],
                    nonces: Sequence[int]) -> List[Tuple[int, GenericProof]]:
     """DirectDecryptionAndProof per text: M_i = A^{s_i} + generic CP proof

@@ -111,3 +111,26 @@ def test_verify_shares_large_batch_key_table(group):
     mixed = Ki.copy()
     mixed[5] = np.frombuffer(p_bytes(gk[1].public_key), np.uint8)  # wrong key for share 5 -> window path
     assert verify(mixed) == [5, 17, 8199]
+
+
+def test_share_backups_gpu_ceremony_and_trustee(group):
+    """GPU key ceremony backups decrypt (oracle, CPython) to P_l(x_i); the trustee's
+    share_of() opens them on the GPU; a tampered backup makes compensatedDecrypt fail."""
+    from electionguard.decrypt import DecryptingTrustee
+    from electionguard.keyceremony import backup_label, key_ceremony
+    og = O.production_group()
+    gk, K = key_ceremony(group, 4, 3, seed=91)
+    for gi in gk:
+        for gl in gk:
+            if gl.gid == gi.gid:
+                continue
+            share = O.poly_eval(gl.coeffs, gi.x, og.q)
+            assert O.backup_decrypt(og, gi.secret, gi.backups_from[gl.gid], backup_label(gl.gid, gi.gid)) == share
+    comm = {g.gid: g.commitments for g in gk}
+    t = DecryptingTrustee(group, gk[0], comm)
+    assert t.share_of(gk[2].gid) == O.poly_eval(gk[2].coeffs, gk[0].x, og.q)
+    c0, c1, c2 = gk[1].backups_from[gk[3].gid]
+    gk[1].backups_from[gk[3].gid] = (c0, c1, bytes([c2[0] ^ 0x80]) + c2[1:])
+    t1 = DecryptingTrustee(group, gk[1], comm)
+    with pytest.raises(ValueError):
+        t1.compensatedDecrypt(group, gk[3].gid, np.zeros((1, 2, 512), np.uint8), 5)

@@ -66,3 +66,27 @@ def test_tally_group_layout_matches_oracle_order():
             for c in range(2):
                 row = g[(k * 3 + s) * 2 + c]
                 assert list(row) == [cts[b, k * man.spc + s, c] for b in range(nb)]
+
+
+def test_share_backup_kdf_matches_oracle():
+    """The product's backup KDF/MAC (keyceremony.backup_open, host code) opens backups made by
+    the oracle restatement, rejects a flipped bit and a wrong recipient (CPU only: k = c0^s by
+    CPython pow)."""
+    import random
+    import eg_oracle as O
+    from electionguard.keyceremony import backup_label, backup_open
+    G = O.production_group()
+    rng = random.Random(31)
+    gs, _ = O.key_ceremony(G, 3, 2, rng)
+    for l, i in [(0, 1), (2, 0)]:
+        share = O.poly_eval(gs[l].coeffs, gs[i].x, G.q)
+        label = backup_label(gs[l].gid, gs[i].gid)
+        c0, c1, c2 = O.backup_encrypt(G, gs[i].K, share, rng.randrange(1, G.q), label)
+        k = pow(c0, gs[i].s, G.p)
+        assert backup_open(c0, k, c1, c2, label) == share
+        assert O.backup_decrypt(G, gs[i].s, (c0, c1, c2), label) == share
+        bad = bytes([c1[0] ^ 1]) + c1[1:]
+        assert backup_open(c0, k, bad, c2, label) is None
+        wrong = gs[(i + 1) % 3]
+        assert backup_open(c0, pow(c0, wrong.s, G.p), c1, c2, label) is None
+        assert backup_open(c0, k, c1, c2, backup_label(gs[l].gid, wrong.gid)) is None
