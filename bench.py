@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--fb-window", type=int, default=22, help="fixed-base radix window bits for g and K")
     ap.add_argument("--cpu-sample", type=int, default=256, help="ballots for the CPU baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--modexp-n", type=int, default=1 << 20,
+                    help="modexp microbenchmark batch per GPU (SURVEY 8(d): 2^20; 0 = skip)")
     return ap.parse_args()
 
 
@@ -97,6 +99,9 @@ def main():
     d_okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
     d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
+    # modexp/sec/GPU microbenchmark, run before the verify step so the verify
+    # launches stay the last k_pow dispatches of the process (tools/prof_summary.py)
+    modexp = modexp_ubench(group, a.modexp_n, dev, rank) if a.modexp_n > 0 else None
     ver = Verifier(group, key, qbar, man)
     final_tally = None
 
@@ -188,6 +193,7 @@ def main():
         "modexp_var_base_per_s_per_gpu": round((4 * man.nsel + 2 * man.n_contests) * value / world, 1),
         "modexp_fixed_base_per_s_per_gpu": round((5 * man.nsel + 3 * man.n_contests) * value / world, 1),
         "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
+        "modexp_ubench": modexp,
         "build": build_id,
     }
     # HBM traffic of k_pow from the committed PMC passes of this same command
@@ -209,6 +215,54 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def modexp_ubench(group, n, dev, rank, reps=2):
+    """SURVEY 8(d) modexp microbenchmark on one GPU: n variable-base powP (bases g^x, x and the
+    exponents uniform in [1, q)) and n fixed-base gPowP, operands resident in HBM
+    (eg_powp_batch_dev / eg_fb_pow_batch_dev); a few results are spot-checked with CPython pow."""
+    import torch
+
+    rng = np.random.default_rng(7 + rank)
+    q, p, g = group.q, group.p, group.g
+
+    def scalars(m):  # uniform 256-bit: in [1, q) except with probability 2^-248 (used as given)
+        return rng.integers(0, 256, size=(m, 32), dtype=np.uint8)
+
+    xs = torch.from_numpy(scalars(n)).to(dev)
+    es = torch.from_numpy(scalars(n)).to(dev)
+    bases = torch.empty((n, 512), dtype=torch.uint8, device=dev)
+    out = torch.empty((n, 512), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    group.gPowP_batch_dev(xs.data_ptr(), bases.data_ptr(), n)  # bases g^x (subgroup elements)
+    group.powP_batch_dev(bases.data_ptr(), es.data_ptr(), out.data_ptr(), n)  # warm-up (job table)
+    group.sync()
+    res = {"n": n, "exponent_bits": 256, "reps": reps}
+    for name, run in (("var_base", lambda: group.powP_batch_dev(bases.data_ptr(), es.data_ptr(), out.data_ptr(), n)),
+                      ("fixed_base_g", lambda: group.gPowP_batch_dev(es.data_ptr(), out.data_ptr(), n))):
+        run()
+        group.sync()
+        group.profile_begin()
+        t = time.perf_counter()
+        for _ in range(reps):
+            run()
+        group.sync()
+        el = time.perf_counter() - t
+        kp = group.profile_end()
+        res[f"{name}_per_s"] = round(n * reps / el, 1)
+        res[f"{name}_mont_ops_per_exp"] = round(kp.mont_ops / (n * reps), 1)
+        res[f"{name}_kpow_tmac_s"] = round(kp.macs / (kp.ms / 1e3) / 1e12, 3) if kp.ms > 0 else None
+        # spot check the last run's first and last results (CPython pow; not the oracle)
+        ob, xb, eb_ = out.cpu().numpy(), xs.cpu().numpy(), es.cpu().numpy()
+        for i in (0, n - 1):
+            e = int.from_bytes(eb_[i].tobytes(), "big")
+            b = pow(g, int.from_bytes(xb[i].tobytes(), "big"), p) if name == "var_base" else g
+            if int.from_bytes(ob[i].tobytes(), "big") != pow(b, e, p):
+                raise RuntimeError(f"modexp microbenchmark {name}: result {i} differs from pow()")
+    res["spot_checked"] = True
+    del xs, es, bases, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline(a, man, eb, qbar, K, gpu_tally):

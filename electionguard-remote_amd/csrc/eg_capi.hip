@@ -668,3 +668,72 @@ extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr
 }
 
 #include "eg_capi_ballot.inc"
+
+// ------------------------------------------------------------------------------
+// device-pointer powP / fixed-base powP (asynchronous on the ctx stream): the
+// resident-operand form of eg_powp_batch / eg_fb_pow_batch for callers that keep
+// elements in HBM across calls (the modexp microbenchmark).  The
+// identity job table of a batch size is built once and cached like the verify tables.
+// ------------------------------------------------------------------------------
+static int identity_pow_jobs(eg_ctx* c, size_t n, bool fbonly, const uint32_t** out) {
+  const std::string key = std::string(fbonly ? "fb/" : "pw/") + std::to_string(n);
+  if (c->cache.find(key) == c->cache.end() && c->cache.size() >= 64) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (auto& kv : c->cache) HIPCHK(hipFree(kv.second.ptr));
+    c->cache.clear();
+  }
+  if (c->cache.find(key) == c->cache.end()) {
+    auto jobs = new_jobs(n);
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t* J = &jobs[i * kJobWords];
+      J[0] = fbonly ? kNone : (uint32_t)i;
+      J[1] = (uint32_t)i;
+      J[3] = (uint32_t)i;
+      J[5] = (uint32_t)i;
+    }
+    return cached_jobs(c, key, jobs, out);
+  }
+  *out = (const uint32_t*)c->cache[key].ptr;
+  return EG_OK;
+}
+
+static int pow_dev(eg_ctx* c, const uint8_t* d_base_be, const uint8_t* d_exp_be, uint8_t* d_out_be, size_t n,
+                   const FbTab* fbonly) {
+  if (n > ((size_t)1 << 31)) return fail(EG_ERR_ARG, "batch too large");
+  const uint32_t* d_jobs = nullptr;
+  uint32_t *d_e = nullptr, *d_o = nullptr;
+  int rc;
+  if ((rc = identity_pow_jobs(c, n, fbonly != nullptr, &d_jobs))) return rc;
+  PowShape S{};
+  S.nout = 1;
+  S.exp_bytes = 32;
+  if (fbonly) {
+    S.nfb[0] = 1;
+    S.tab[0][0] = 0;
+  } else {
+    S.has_base = 1;
+    if ((rc = ws_get(c, W_E0, n * kW * 4, (void**)&d_e))) return rc;
+    if ((rc = launch_import(c, d_base_be, n, d_e, nullptr))) return rc;
+  }
+  if ((rc = ws_get(c, W_E1, n * kW * 4, (void**)&d_o))) return rc;
+  FbTab f0 = fbonly ? *fbonly : c->gtab->tab();
+  if ((rc = launch_pow(c, S, d_jobs, n, d_e, d_exp_be, d_o, f0, f0))) return rc;
+  return launch_export(c, d_o, n, d_out_be);
+}
+
+extern "C" int eg_powp_batch_dev(eg_ctx* c, const uint8_t* d_base_be, const uint8_t* d_exp_be, uint8_t* d_out_be,
+                                 size_t n) {
+  if (!c || (n && (!d_base_be || !d_exp_be || !d_out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!n) return EG_OK;
+  Locked L(c);
+  return pow_dev(c, d_base_be, d_exp_be, d_out_be, n, nullptr);
+}
+
+extern "C" int eg_fb_pow_batch_dev(eg_fixed_base* fb, const uint8_t* d_exp_be, uint8_t* d_out_be, size_t n) {
+  if (!fb || (n && (!d_exp_be || !d_out_be))) return fail(EG_ERR_ARG, "null argument");
+  if (!n) return EG_OK;
+  eg_ctx* c = fb->ctx;
+  Locked L(c);
+  FbTab t = fb->tab();
+  return pow_dev(c, nullptr, d_exp_be, d_out_be, n, &t);
+}

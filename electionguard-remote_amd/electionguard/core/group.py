@@ -147,6 +147,19 @@ class GroupContext:
                          self._lib.eg_fb_pow_batch(fb, _ptr(E), _ptr(out), len(E)))
         return out
 
+    def powP_batch_dev(self, d_bases: int, d_exps: int, d_out: int, n: int) -> None:
+        """Asynchronous powP on device pointers (n x 512 B bases, n x 32 B exponents, n x 512 B
+        out, big-endian rows in HBM, e.g. torch CUDA tensors' data_ptr()); ``sync()`` waits."""
+        if n:
+            native.check(self._lib, "eg_powp_batch_dev",
+                         self._lib.eg_powp_batch_dev(self._ctx, d_bases, d_exps, d_out, n))
+
+    def gPowP_batch_dev(self, d_exps: int, d_out: int, n: int) -> None:
+        """Asynchronous gPowP on device pointers (see powP_batch_dev)."""
+        if n:
+            fb = self._lib.eg_ctx_g_table(self._ctx)
+            native.check(self._lib, "eg_fb_pow_batch_dev", self._lib.eg_fb_pow_batch_dev(fb, d_exps, d_out, n))
+
     def multP_batch(self, a, b) -> np.ndarray:
         A, B = as_p_array(a), as_p_array(b)
         if len(A) != len(B):
@@ -229,6 +242,12 @@ class FixedBase:
             native.check(self.group._lib, "eg_fb_pow_batch",
                          self.group._lib.eg_fb_pow_batch(self._fb, _ptr(E), _ptr(out), len(E)))
         return out
+
+    def pow_batch_dev(self, d_exps: int, d_out: int, n: int) -> None:
+        """Asynchronous base^exps[i] on device pointers (see GroupContext.powP_batch_dev)."""
+        if n:
+            native.check(self.group._lib, "eg_fb_pow_batch_dev",
+                         self.group._lib.eg_fb_pow_batch_dev(self._fb, d_exps, d_out, n))
 
     def close(self) -> None:
         if getattr(self, "_fb", None):

@@ -20,6 +20,7 @@ EXPORTED = [
     "eg_last_error", "eg_version", "eg_ctx_create", "eg_ctx_destroy", "eg_ctx_sync",
     "eg_ctx_profile_begin", "eg_ctx_profile_end", "eg_ctx_g_table",
     "eg_fixed_base_create", "eg_fixed_base_destroy", "eg_powp_batch", "eg_fb_pow_batch",
+    "eg_powp_batch_dev", "eg_fb_pow_batch_dev",
     "eg_multp_batch", "eg_prod_reduce", "eg_multinv_batch", "eg_verify_ballots",
     "eg_set_election_key", "eg_verify_ballots_dev", "eg_encrypt_ballots",
     "eg_trustee_decrypt_batch", "eg_verify_shares",
@@ -62,6 +63,8 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_fixed_base_destroy": ([P], I),
         "eg_powp_batch": ([P, P, P, P, S], I),
         "eg_fb_pow_batch": ([P, P, P, S], I),
+        "eg_powp_batch_dev": ([P, P, P, P, S], I),
+        "eg_fb_pow_batch_dev": ([P, P, P, S], I),
         "eg_multp_batch": ([P, P, P, P, S], I),
         "eg_prod_reduce": ([P, P, S, S, P], I),
         "eg_multinv_batch": ([P, P, P, S], I),

@@ -91,6 +91,12 @@ int eg_powp_batch(eg_ctx* ctx, const uint8_t* base_be, const uint8_t* exp_be,
                   uint8_t* out_be, size_t n);
 /* Fixed-base powP (gPowP / accelerated K.powP): out[i] = base^exp[i] mod p. */
 int eg_fb_pow_batch(eg_fixed_base* fb, const uint8_t* exp_be, uint8_t* out_be, size_t n);
+/* Same two, device pointers (512 B / 32 B big-endian rows in HBM), asynchronous on
+ * the ctx stream (eg_ctx_sync to wait): for callers that keep elements resident
+ * across calls, e.g. the modexp-per-second microbenchmark. */
+int eg_powp_batch_dev(eg_ctx* ctx, const uint8_t* d_base_be, const uint8_t* d_exp_be,
+                      uint8_t* d_out_be, size_t n);
+int eg_fb_pow_batch_dev(eg_fixed_base* fb, const uint8_t* d_exp_be, uint8_t* d_out_be, size_t n);
 /* ElementModP.times: out[i] = a[i] * b[i] mod p. */
 int eg_multp_batch(eg_ctx* ctx, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be,
                    size_t n);

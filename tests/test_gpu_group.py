@@ -102,3 +102,39 @@ def test_generic_odd_modulus(oracle_group):
     for i in range(20):
         assert be2i(gout[i]) == pow(g, exps[i], p), i
     G.close()
+
+
+def test_powp_and_fb_dev_pointers(group, oracle_group):
+    """eg_powp_batch_dev / eg_fb_pow_batch_dev (operands resident in HBM, torch tensors'
+    data_ptr()): same results as the host-pointer calls and the oracle, incl. edge cases,
+    a ragged size and a second call that reuses the cached job table."""
+    import torch
+    O = oracle_group
+    rng = random.Random(23)
+    p, q = O.p, O.q
+    bases = [0, 0, 1, p - 1, p, p + 1, 2**4096 - 1, O.g] + [rng.randrange(2**4096) for _ in range(91)]
+    exps = [0, 5, 2**256 - 1, 2, 7, 3, 2**256 - 1, q] + [rng.randrange(2**256) for _ in range(91)]
+    n = len(bases)
+    B = np.stack([np.frombuffer(b.to_bytes(512, "big"), np.uint8) for b in bases])
+    E = np.stack([np.frombuffer(e.to_bytes(32, "big"), np.uint8) for e in exps])
+    dB, dE = torch.from_numpy(B).cuda(), torch.from_numpy(E).cuda()
+    dO = torch.zeros((n, 512), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        dO.zero_()
+        group.powP_batch_dev(dB.data_ptr(), dE.data_ptr(), dO.data_ptr(), n)
+        group.sync()
+        out = dO.cpu().numpy()
+        for i in range(n):
+            assert be2i(out[i]) == O.powP(bases[i], exps[i]), i
+    group.gPowP_batch_dev(dE.data_ptr(), dO.data_ptr(), n)
+    group.sync()
+    out = dO.cpu().numpy()
+    for i in range(n):
+        assert be2i(out[i]) == O.gPowP(exps[i]), i
+    fb = group.fixed_base(bases[20], window_bits=9)
+    fb.pow_batch_dev(dE.data_ptr(), dO.data_ptr(), 33)
+    group.sync()
+    out = dO.cpu().numpy()
+    for i in range(33):
+        assert be2i(out[i]) == O.powP(bases[20], exps[i]), i
+    fb.close()
