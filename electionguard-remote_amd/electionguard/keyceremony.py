@@ -19,7 +19,8 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
-from .core.group import GroupContext, p_bytes
+from .core.group import GroupContext, as_p_array, p_bytes
+from .core.hashing import hash_elems
 
 
 @dataclass
@@ -30,6 +31,7 @@ class GuardianKeys:
     commitments: List[int]                       # g^{a_j}
     shares_from: Dict[str, int] = field(default_factory=dict)  # l -> P_l(x)
     backups_from: Dict[str, Tuple[int, bytes, bytes]] = field(default_factory=dict)  # l -> (c0, c1, c2)
+    proofs: List[Tuple[int, int]] = field(default_factory=list)  # Schnorr (c, v) per commitment
 
     @property
     def secret(self) -> int:
@@ -101,6 +103,61 @@ def key_ceremony(group: GroupContext, n: int, quorum: int, seed: Optional[int] =
             stream, mac_key = backup_keys(c0, k, label)
             c1 = bytes(a ^ b for a, b in zip(gi.shares_from[gl.gid].to_bytes(32, "big"), stream))
             gi.backups_from[gl.gid] = (c0, c1, hmac.new(mac_key, p_bytes(c0) + c1, hashlib.sha256).digest())
+    # Schnorr proofs of every coefficient (h = g^u on the GPU, hash on the host)
+    us = [draw() for _ in flat]
+    hs = group.gPowP_batch(us)
+    for i, gi in enumerate(gs):
+        for j in range(quorum):
+            k = i * quorum + j
+            c = hash_elems(q, ("P", gi.commitments[j]), ("P", int.from_bytes(hs[k].tobytes(), "big")))
+            gi.proofs.append((c, (us[k] - c * gi.coeffs[j]) % q))
     Ks = np.stack([np.frombuffer(p_bytes(g.public_key), dtype=np.uint8) for g in gs])
     K = int.from_bytes(group.prodP_groups(Ks, 1, n)[0].tobytes(), "big")
     return gs, K
+
+
+def _be(row) -> int:
+    return int.from_bytes(row.tobytes(), "big")
+
+
+def verify_commitment_proofs(group: GroupContext, commitments: List[int], proofs: List[Tuple[int, int]]) -> List[bool]:
+    """Schnorr proofs of the public commitments K_ij (what each guardian checks of the others
+    in the key ceremony), one GPU batch: K^q == 1, h = g^v K^c, c == H(K, h).  Same
+    definition as oracle/eg_oracle.py (schnorr_verify)."""
+    n = len(commitments)
+    if len(proofs) != n:
+        raise ValueError("one proof per commitment")
+    if not n:
+        return []
+    q, p = group.q, group.p
+    Ks = as_p_array(commitments)
+    res = group.powP_batch(np.concatenate([Ks, Ks]), [q] * n + [c for c, _ in proofs])
+    h = group.multP_batch(group.gPowP_batch([v for _, v in proofs]), res[n:])
+    out = []
+    for k in range(n):
+        c, v = proofs[k]
+        K = commitments[k]
+        ok = 0 < K < p and 0 <= c < q and 0 <= v < q and _be(res[k]) == 1
+        out.append(bool(ok and c == hash_elems(q, ("P", K), ("P", _be(h[k])))))
+    return out
+
+
+def verify_backups(group: GroupContext, keys: GuardianKeys, all_commitments: Dict[str, List[int]]) -> Dict[str, bool]:
+    """A recipient's check of every backup it holds (key ceremony, receiving side): the backup
+    opens under its secret (k = c0^{s_i}, one GPU batch) and the share matches the sender's
+    commitments, g^{P_l(x_i)} == prod_j K_lj^{x_i^j} (two GPU batches + one product)."""
+    ids = sorted(keys.backups_from)
+    if not ids:
+        return {}
+    q = group.q
+    ks = group.powP_batch([keys.backups_from[l][0] for l in ids], [keys.secret] * len(ids))
+    shares = [backup_open(keys.backups_from[l][0], _be(ks[t]), keys.backups_from[l][1], keys.backups_from[l][2],
+                          backup_label(l, keys.gid)) for t, l in enumerate(ids)]
+    quorum = len(all_commitments[ids[0]])
+    if any(len(all_commitments[l]) != quorum for l in ids):
+        raise ValueError("all guardians commit to quorum coefficients")
+    xe = [pow(keys.x, j, q) for j in range(quorum)]
+    terms = group.powP_batch([K for l in ids for K in all_commitments[l]], xe * len(ids))
+    rk = group.prodP_groups(terms, len(ids), quorum)
+    gs = group.gPowP_batch([s if s is not None else 0 for s in shares])
+    return {l: shares[t] is not None and _be(gs[t]) == _be(rk[t]) for t, l in enumerate(ids)}

@@ -401,6 +401,35 @@ def backup_decrypt(G: Group, s_to: int, backup: Tuple[int, bytes, bytes], label:
     return int.from_bytes(bytes(a ^ b for a, b in zip(c1, stream)), "big")
 
 
+# --------------------------------------------------------------------------------------
+# Key-ceremony proofs (RunRemoteKeyCeremony.java:200-233 and
+# RunRemoteTrustee.java:184 reach them through upstream KeyCeremonyTrustee):
+#  * Schnorr proof of knowledge of each coefficient a_ij behind K_ij = g^{a_ij}, compact
+#    (c, v) like the other proofs: h = g^u, c = H(K_ij, h), v = u - c*a_ij mod q;
+#    verify: K_ij^q == 1 (valid residue), h = g^v K_ij^c, c == H(K_ij, h);
+#  * a recipient checks a decrypted backup share against the sender's commitments:
+#    g^{P_l(x_i)} == prod_j K_lj^{x_i^j} (= recovery_public_key).
+# The upstream pre-image (domain labels) is not in the container: unpinned, and defined
+# identically here and in electionguard/keyceremony.py.
+# --------------------------------------------------------------------------------------
+
+def schnorr_prove(G: Group, a: int, K: int, u: int) -> GenericProof:
+    h = G.gPowP(u)
+    c = hash_elems(G.q, ("P", K), ("P", h))
+    return GenericProof(c, (u - c * a) % G.q)
+
+
+def schnorr_verify(G: Group, K: int, pr: GenericProof) -> bool:
+    if not (0 < K < G.p) or G.powP(K, G.q) != 1 or not (0 <= pr.c < G.q and 0 <= pr.v < G.q):
+        return False
+    h = G.multP(G.gPowP(pr.v), G.powP(K, pr.c))
+    return pr.c == hash_elems(G.q, ("P", K), ("P", h))
+
+
+def verify_backup_share(G: Group, share: int, sender: Guardian, x: int) -> bool:
+    return G.gPowP(share) == recovery_public_key(G, sender, x)
+
+
 def direct_decrypt(G: Group, qbar: int, gd: Guardian, texts: Sequence[Ciphertext],
                    nonces: Sequence[int]) -> List[Tuple[int, GenericProof]]:
     """DirectDecryptionAndProof per text: M_i = A^{s_i} + generic CP proof

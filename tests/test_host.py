@@ -90,3 +90,22 @@ def test_share_backup_kdf_matches_oracle():
         wrong = gs[(i + 1) % 3]
         assert backup_open(c0, pow(c0, wrong.s, G.p), c1, c2, label) is None
         assert backup_open(c0, k, c1, c2, backup_label(gs[l].gid, wrong.gid)) is None
+
+
+def test_oracle_schnorr_and_backup_checks():
+    """Oracle restatement of the key-ceremony proofs (CPU, CPython pow): prove -> verify,
+    tampering and non-residues rejected; backup shares checked against commitments."""
+    import random
+    import eg_oracle as O
+    G = O.production_group()
+    rng = random.Random(8)
+    gs, _ = O.key_ceremony(G, 3, 2, rng)
+    a, K = gs[1].coeffs[1], gs[1].commitments[1]
+    pr = O.schnorr_prove(G, a, K, rng.randrange(1, G.q))
+    assert O.schnorr_verify(G, K, pr)
+    assert not O.schnorr_verify(G, K, O.GenericProof(pr.c, (pr.v + 1) % G.q))
+    assert not O.schnorr_verify(G, G.p - 1, pr)
+    assert not O.schnorr_verify(G, gs[0].K, pr)
+    share = O.poly_eval(gs[2].coeffs, gs[0].x, G.q)
+    assert O.verify_backup_share(G, share, gs[2], gs[0].x)
+    assert not O.verify_backup_share(G, share, gs[2], gs[1].x)

@@ -1,7 +1,8 @@
 """End-to-end remote workflow — ``RunRemoteWorkflowTest.main``
 (src/test/java/electionguard/workflow/RunRemoteWorkflowTest.java:83-192) on the GPU path:
 
-  1 key ceremony (synthetic, in-process)   2 encrypt ballots (GPU)
+  1 key ceremony (in-process; commitments, Schnorr proofs and share backups made and
+    checked on the GPU)                     2 encrypt ballots (GPU)
   3 accumulate tally + verify ballots (GPU)
   4 remote decryption: one trustee PROCESS per available guardian over gRPC on localhost,
     missing guardians compensated (RunRemoteDecryptionTest.java:63-136)
@@ -36,14 +37,21 @@ def main():
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
     from electionguard.core import productionGroup
     from electionguard.decrypt import Decryption
-    from electionguard.keyceremony import key_ceremony
+    from electionguard.keyceremony import key_ceremony, verify_backups, verify_commitment_proofs
     from electionguard.remote import RemoteDecryptingTrusteeProxy
     from electionguard.trustee_server import write_trustee_file
 
     t_all = time.time()
     G = productionGroup(0)
     navail = a.navailable or a.quorum
+    t = time.time()
     gk, K = key_ceremony(G, a.nguardians, a.quorum)
+    comm = {g.gid: g.commitments for g in gk}
+    kc_ok = all(verify_commitment_proofs(G, [k for g in gk for k in g.commitments], [pr for g in gk for pr in g.proofs]))
+    kc_ok = kc_ok and all(all(verify_backups(G, g, comm).values()) for g in gk)
+    print(f"*** keyCeremony {a.nguardians} guardians quorum {a.quorum} {time.time() - t:.3f} s, proofs+backups valid = {kc_ok}")
+    if not kc_ok:
+        return 1
     key = ElectionKey(G, K)
     qbar = int.from_bytes(os.urandom(32), "big") % G.q
     man = Manifest(4, 5, 1)
@@ -57,7 +65,6 @@ def main():
     ok_s, ok_c, tally = Verifier(G, key, qbar, man).verify(eb)
     print(f"*** verify+accumTally {time.time() - t:.3f} s, all valid = {bool(ok_s.all() and ok_c.all())}")
     tmp = Path(tempfile.mkdtemp(prefix="eg_trustees_"))
-    comm = {g.gid: g.commitments for g in gk}
     procs, proxies = [], []
     try:
         for k, g in enumerate(gk[:navail]):
