@@ -64,16 +64,14 @@ def random_scalars(rng: np.random.Generator, shape, q: int) -> np.ndarray:
     out = rng.integers(0, 256, size=tuple(shape) + (32,), dtype=np.uint8)
     flat = out.reshape(-1, 32)
     qb = np.frombuffer(q_bytes(q), dtype=np.uint8)
-    # rows >= q are re-drawn (probability ~2^-248 for the EG q)
+    q_top = int.from_bytes(bytes(qb[:8]), "big")
+    # rows >= q are re-drawn (probability ~2^-248 for the EG q).  The top 64 bits decide every
+    # row except those equal to q's top word, which are compared byte by byte.
     while True:
-        ge = np.zeros(len(flat), dtype=bool)
-        undecided = np.ones(len(flat), dtype=bool)
-        for k in range(32):
-            gt = undecided & (flat[:, k] > qb[k])
-            lt = undecided & (flat[:, k] < qb[k])
-            ge |= gt
-            undecided &= ~(gt | lt)
-        ge |= undecided  # equal to q
+        top = flat[:, :8].copy().view(">u8").ravel()
+        ge = top > q_top
+        for i in np.flatnonzero(top == q_top):
+            ge[i] = bytes(flat[i]) >= bytes(qb)
         if not ge.any():
             return out
         flat[ge] = rng.integers(0, 256, size=(int(ge.sum()), 32), dtype=np.uint8)

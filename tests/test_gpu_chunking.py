@@ -79,3 +79,28 @@ def test_two_chunks_tally_combined(group):
     rp[17000, 1, 3, 5] ^= 0x02
     ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, eb.cproof), with_tally=False)
     assert np.argwhere(~ok_s).tolist() == [[17000, 1]] and ok_c.all()
+
+
+def test_encrypt_chunk_boundary(group):
+    """eg_encrypt_ballots runs in 16384-ballot chunks: with injected nonces the bytes of a
+    ballot must not depend on which chunk it lands in (ballots straddling the boundary are
+    re-encrypted alone and compared), and every proof verifies."""
+    from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
+    from electionguard.keyceremony import key_ceremony
+    man = Manifest(1, 2, 1)
+    nb = 16384 + 5
+    _, K = key_ceremony(group, 3, 3, seed=53)
+    key = ElectionKey(group, K, window_bits=12)
+    rng = np.random.default_rng(53)
+    votes = random_votes(rng, man, nb)
+    sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
+    cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    qbar = 9091
+    eb = batch_encryption(group, key, qbar, man, votes, sn, cn)
+    a, b = 16380, nb
+    part = batch_encryption(group, key, qbar, man, votes[a:b], sn[a:b], cn[a:b])
+    assert np.array_equal(part.cts, eb.cts[a:b])
+    assert np.array_equal(part.rproof, eb.rproof[a:b])
+    assert np.array_equal(part.cproof, eb.cproof[a:b])
+    ok_s, ok_c, _ = Verifier(group, key, qbar, man).verify(eb, with_tally=False)
+    assert ok_s.all() and ok_c.all()

@@ -10,6 +10,8 @@
 
     python tools/run_workflow.py -nguardians 3 -quorum 3 -nballots 25            # configs[0]
     python tools/run_workflow.py -nguardians 5 -quorum 3 -navailable 3 -nballots 100   # configs[3]
+    python tools/run_workflow.py -nballots 1000000                                      # configs[2] tally size
+    python tools/run_workflow.py -ncontests 20 -nballots 1000000                        # configs[4] manifest
 """
 import argparse
 import json
@@ -33,6 +35,11 @@ def main():
     ap.add_argument("-navailable", type=int, default=0)
     ap.add_argument("-nballots", type=int, default=25)
     ap.add_argument("-ngpus", type=int, default=1, help="trustee k runs on GPU k % ngpus")
+    ap.add_argument("-ncontests", type=int, default=4)
+    ap.add_argument("-nselections", type=int, default=5, help="real selections per contest (+1 placeholder)")
+    ap.add_argument("-fbwindow", type=int, default=8, help="fixed-base radix window bits for K (8 = LOW_MEMORY_USE)")
+    ap.add_argument("-chunk", type=int, default=65536,
+                    help="ballots per encrypt+verify batch; batch tallies are multiplied (bounded memory)")
     a = ap.parse_args()
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
     from electionguard.core import productionGroup
@@ -52,18 +59,35 @@ def main():
     print(f"*** keyCeremony {a.nguardians} guardians quorum {a.quorum} {time.time() - t:.3f} s, proofs+backups valid = {kc_ok}")
     if not kc_ok:
         return 1
-    key = ElectionKey(G, K)
+    key = ElectionKey(G, K, window_bits=a.fbwindow)
     qbar = int.from_bytes(os.urandom(32), "big") % G.q
-    man = Manifest(4, 5, 1)
+    man = Manifest(a.ncontests, a.nselections, 1)
     rng = np.random.default_rng()
-    votes = random_votes(rng, man, a.nballots)
-    t = time.time()
-    eb = batch_encryption(G, key, qbar, man, votes, random_scalars(rng, (a.nballots, man.nsel, 4), G.q),
-                          random_scalars(rng, (a.nballots, man.n_contests), G.q))
-    print(f"*** encryptBallots {a.nballots} ballots {time.time() - t:.3f} s")
-    t = time.time()
-    ok_s, ok_c, tally = Verifier(G, key, qbar, man).verify(eb)
-    print(f"*** verify+accumTally {time.time() - t:.3f} s, all valid = {bool(ok_s.all() and ok_c.all())}")
+    ver = Verifier(G, key, qbar, man)
+    expected = np.zeros(man.n_real, dtype=np.int64)
+    tally, t_enc, t_ver, t_gen, all_ok = None, 0.0, 0.0, 0.0, True
+    for b0 in range(0, a.nballots, a.chunk):
+        nb = min(a.chunk, a.nballots - b0)
+        t = time.time()
+        votes = random_votes(rng, man, nb)
+        sn = random_scalars(rng, (nb, man.nsel, 4), G.q)
+        cn = random_scalars(rng, (nb, man.n_contests), G.q)
+        expected += votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].sum(axis=0, dtype=np.int64).reshape(-1)
+        t_gen += time.time() - t
+        t = time.time()
+        eb = batch_encryption(G, key, qbar, man, votes, sn, cn)
+        t_enc += time.time() - t
+        t = time.time()
+        ok_s, ok_c, part = ver.verify(eb)
+        all_ok = all_ok and bool(ok_s.all() and ok_c.all())
+        tally = part if tally is None else G.multP_batch(tally.reshape(-1, 512), part.reshape(-1, 512)).reshape(part.shape)
+        t_ver += time.time() - t
+        if a.nballots > a.chunk:
+            print(f"    {b0 + nb}/{a.nballots} ballots: encrypt {t_enc:.1f} s, verify+tally {t_ver:.1f} s", flush=True)
+    print(f"*** encryptBallots {a.nballots} ballots ({man.nsel} selections each) {t_enc:.3f} s "
+          f"({a.nballots / max(t_enc, 1e-9):.0f} ballots/s; host nonce generation {t_gen:.1f} s untimed)")
+    print(f"*** verify+accumTally {t_ver:.3f} s ({a.nballots / max(t_ver, 1e-9):.0f} ballots/s), all valid = {all_ok}",
+          flush=True)
     tmp = Path(tempfile.mkdtemp(prefix="eg_trustees_"))
     procs, proxies = [], []
     try:
@@ -83,7 +107,6 @@ def main():
         dec = Decryption(G, qbar, proxies, [g.gid for g in gk[navail:]], {g.gid: g.public_key for g in gk})
         counts = dec.decrypt(tally, a.nballots)
         print(f"*** remote decryption ({navail} trustees, {a.nguardians - navail} missing) {time.time() - t:.3f} s")
-        expected = votes.reshape(a.nballots, man.n_contests, man.spc)[:, :, : man.n_selections].sum(axis=0).reshape(-1)
         ok = counts == [int(x) for x in expected]
         print(json.dumps({"counts": counts, "expected": [int(x) for x in expected], "match": ok,
                           "all_took_s": round(time.time() - t_all, 3)}))
@@ -91,7 +114,7 @@ def main():
             px.finish(ok)
         for p in procs:
             p.wait(timeout=60)
-        return 0 if ok and ok_s.all() and ok_c.all() else 1
+        return 0 if ok and all_ok else 1
     finally:
         for p in procs:
             if p.poll() is None:
