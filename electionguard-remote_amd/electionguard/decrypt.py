@@ -215,6 +215,19 @@ def dlog_g_batch(group: GroupContext, ys, max_result: int) -> List[Optional[int]
     return out
 
 
+@dataclass
+class DecryptionRecord:
+    """What the mediator publishes for a decrypted tally (the EG 1.0 DecryptionShare data the
+    reference's ``Verifier.verify`` re-checks, RunRemoteWorkflowTest.java:179-182):
+    per text, every available guardian's direct share, every (missing, available) pair's
+    compensated share with its recovery key, and the plaintext counts."""
+    texts: np.ndarray                                            # (n, 2, 512) encrypted tally
+    xs: Dict[str, int]                                           # available guardian -> x coordinate
+    direct: Dict[str, List[DirectDecryptionAndProof]]            # available guardian -> n shares
+    compensated: Dict[str, Dict[str, List[CompensatedDecryptionAndProof]]]  # missing -> available -> n
+    counts: List[Optional[int]]
+
+
 class Decryption:
     """Mediator combine (``new Decryption(group, init, trustees, missing).decrypt(tally)``)."""
 
@@ -227,10 +240,15 @@ class Decryption:
 
     def decrypt(self, tally: np.ndarray, max_count: int) -> List[Optional[int]]:
         """tally: (n, 2, 512) encrypted per-selection totals -> plaintext counts."""
+        return self.decrypt_record(tally, max_count).counts
+
+    def decrypt_record(self, tally: np.ndarray, max_count: int) -> DecryptionRecord:
+        """decrypt() keeping every share and proof (the published decryption record)."""
         G = self.group
         T = _texts_array(tally)
         n = len(T)
         xs = [t.xCoordinate() for t in self.trustees]
+        rec = DecryptionRecord(T, {t.id(): t.xCoordinate() for t in self.trustees}, {}, {}, [])
         parts = []  # (n,512) arrays to multiply together
         for tr in self.trustees:
             res = tr.directDecrypt(G, T, self.qbar)
@@ -240,8 +258,10 @@ class Decryption:
                                [r.proof for r in res])
             if not ok.all():
                 raise ValueError(f"invalid direct decryption proof from {tr.id()}")
+            rec.direct[tr.id()] = res
             parts.append(as_p_array([r.partialDecryption for r in res]))
         for l in self.missing:
+            rec.compensated[l] = {}
             for tr in self.trustees:
                 res = tr.compensatedDecrypt(G, l, T, self.qbar)
                 if len(res) != n:
@@ -250,6 +270,7 @@ class Decryption:
                                    [r.partialDecryption for r in res], [r.proof for r in res])
                 if not ok.all():
                     raise ValueError(f"invalid compensated decryption proof from {tr.id()} for {l}")
+                rec.compensated[l][tr.id()] = res
                 w = lagrange(xs, tr.xCoordinate(), G.q)
                 Ml = as_p_array([r.partialDecryption for r in res])
                 parts.append(G.powP_batch(Ml, [w] * n))
@@ -257,4 +278,60 @@ class Decryption:
         stacked = np.ascontiguousarray(np.stack(parts, axis=1)).reshape(n * k, 512)
         M = G.prodP_groups(stacked, n, k)
         Tv = G.multP_batch(np.ascontiguousarray(T[:, 1]), G.multInv_batch(M))
-        return dlog_g_batch(G, Tv, max_count)
+        rec.counts = dlog_g_batch(G, Tv, max_count)
+        return rec
+
+
+def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionRecord, public_keys: Dict[str, int],
+                             commitments: Dict[str, List[int]]) -> Dict[str, bool]:
+    """Record-level checks of the tally decryption (the decryption part of the reference's
+    ``Verifier(record, 11).verify()``, RunRemoteWorkflowTest.java:179-182; EG 1.0 spec
+    verification steps for partial / compensated decryptions and the plaintext tally),
+    independent of the mediator that produced ``rec``; every exponentiation runs on the GPU:
+
+      * ``direct_proofs``      every direct share's proof against the guardian's key K_i;
+      * ``recovery_keys``      every recovery key g^{P_l(x_i)} == prod_j K_{l,j}^{x_i^j},
+                               from the missing guardian's public commitments;
+      * ``compensated_proofs`` every compensated share's proof against its recovery key;
+      * ``quorum``             the shares come from one quorum: for every missing guardian
+                               the same set of available guardians, each with a direct share;
+      * ``tally``              B == M * g^t per text with M = prod_i M_i * prod_l prod_i
+                               M_{l,i}^{w_i} (Lagrange w_i over the available x's) and t
+                               the published count.
+    """
+    G = group
+    T = rec.texts
+    n = len(T)
+    out = {"direct_proofs": True, "recovery_keys": True, "compensated_proofs": True, "quorum": True, "tally": True}
+    avail = list(rec.direct)
+    for gid in avail:
+        res = rec.direct[gid]
+        out["direct_proofs"] &= len(res) == n and bool(
+            verify_shares(G, qbar, [public_keys[gid]] * n, T, [r.partialDecryption for r in res],
+                          [r.proof for r in res]).all())
+    if len(rec.counts) != n or any(c is None for c in rec.counts):
+        out["tally"] = False
+    for l, by_avail in rec.compensated.items():
+        out["quorum"] &= sorted(by_avail) == sorted(avail)
+        comm = commitments[l]
+        for gid, res in by_avail.items():
+            x = rec.xs[gid]
+            exps = [pow(x, j, G.q) for j in range(len(comm))]
+            want = _be_int(G.prodP_groups(G.powP_batch(comm, exps), 1, len(comm))[0])
+            out["recovery_keys"] &= len(res) == n and all(r.recoveredPublicKeyShare == want for r in res)
+            out["compensated_proofs"] &= len(res) == n and bool(
+                verify_shares(G, qbar, [r.recoveredPublicKeyShare for r in res], T,
+                              [r.partialDecryption for r in res], [r.proof for r in res]).all())
+    if not (out["quorum"] and out["tally"] and n):
+        return out
+    xs = [rec.xs[g] for g in avail]
+    parts = [as_p_array([r.partialDecryption for r in rec.direct[g]]) for g in avail]
+    for l, by_avail in rec.compensated.items():
+        for gid in avail:
+            w = lagrange(xs, rec.xs[gid], G.q)
+            parts.append(G.powP_batch(as_p_array([r.partialDecryption for r in by_avail[gid]]), [w] * n))
+    k = len(parts)
+    M = G.prodP_groups(np.ascontiguousarray(np.stack(parts, axis=1)).reshape(n * k, 512), n, k)
+    lhs = G.multP_batch(M, G.gPowP_batch([int(c) for c in rec.counts]))
+    out["tally"] = bool(np.array_equal(lhs, np.ascontiguousarray(T[:, 1])))
+    return out

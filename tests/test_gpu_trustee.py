@@ -62,6 +62,73 @@ def test_full_threshold_decryption(group):
     assert counts == [int(x) for x in expected]
 
 
+def test_decryption_record_verification(group):
+    """Record-level decryption checks (verify_decryption_record): an honest record passes
+    every check; a tampered share, recovery key, count or a missing quorum member fails
+    exactly the check it should.  The tally relation B == M g^t is cross-checked with
+    CPython pow on the honest record."""
+    import copy
+    from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
+    from electionguard.decrypt import (CompensatedDecryptionAndProof, DecryptingTrustee, Decryption,
+                                       verify_decryption_record)
+    from electionguard.keyceremony import key_ceremony
+    gk, K = key_ceremony(group, 5, 3, seed=8)
+    key = ElectionKey(group, K)
+    man = Manifest(1, 3, 1)
+    nr = np.random.default_rng(8)
+    nb = 7
+    votes = random_votes(nr, man, nb)
+    qbar = 4242
+    eb = batch_encryption(group, key, qbar, man, votes, random_scalars(nr, (nb, man.nsel, 4), group.q),
+                          random_scalars(nr, (nb, man.n_contests), group.q))
+    _, _, tally = Verifier(group, key, qbar, man).verify(eb)
+    comm = {g.gid: g.commitments for g in gk}
+    pks = {g.gid: g.public_key for g in gk}
+    avail = [DecryptingTrustee(group, g, comm) for g in (gk[0], gk[2], gk[4])]
+    rec = Decryption(group, qbar, avail, [gk[1].gid, gk[3].gid], pks).decrypt_record(tally, nb)
+    expected = votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].sum(axis=0).reshape(-1)
+    assert rec.counts == [int(x) for x in expected]
+    assert all(verify_decryption_record(group, qbar, rec, pks, comm).values())
+    # CPython cross-check of B = M g^t with M rebuilt from the record's shares
+    og = O.production_group()
+    xs = list(rec.xs.values())
+    for i in range(len(rec.counts)):
+        M = 1
+        for gid, res in rec.direct.items():
+            M = M * res[i].partialDecryption % og.p
+        for l, by in rec.compensated.items():
+            for gid, res in by.items():
+                num = den = 1
+                for xj in xs:
+                    if xj != rec.xs[gid]:
+                        num, den = num * xj % og.q, den * (xj - rec.xs[gid]) % og.q
+                M = M * pow(res[i].partialDecryption, num * pow(den, -1, og.q) % og.q, og.p) % og.p
+        assert M * pow(og.g, rec.counts[i], og.p) % og.p == int.from_bytes(bytes(rec.texts[i, 1]), "big")
+
+    def check(r):
+        return verify_decryption_record(group, qbar, r, pks, comm)
+
+    bad = copy.deepcopy(rec)
+    bad.counts[1] += 1
+    v = check(bad)
+    assert not v["tally"] and v["direct_proofs"] and v["compensated_proofs"]
+    bad = copy.deepcopy(rec)
+    d = bad.direct[gk[2].gid][2]
+    d.partialDecryption = d.partialDecryption * og.g % og.p
+    v = check(bad)
+    assert not v["direct_proofs"] and not v["tally"] and v["compensated_proofs"] and v["recovery_keys"]
+    bad = copy.deepcopy(rec)
+    c = bad.compensated[gk[3].gid][gk[4].gid][0]
+    bad.compensated[gk[3].gid][gk[4].gid][0] = CompensatedDecryptionAndProof(
+        c.partialDecryption, c.proof, c.recoveredPublicKeyShare * og.g % og.p)
+    v = check(bad)
+    assert not v["recovery_keys"] and not v["compensated_proofs"] and v["direct_proofs"] and v["tally"]
+    bad = copy.deepcopy(rec)
+    del bad.compensated[gk[1].gid][gk[0].gid]
+    v = check(bad)
+    assert not v["quorum"] and v["direct_proofs"]
+
+
 def test_verify_shares_rejects_bad_proof(group):
     from electionguard.decrypt import GenericChaumPedersenProof, verify_shares
     og = O.production_group()

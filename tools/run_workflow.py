@@ -43,7 +43,7 @@ def main():
     a = ap.parse_args()
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
     from electionguard.core import productionGroup
-    from electionguard.decrypt import Decryption
+    from electionguard.decrypt import Decryption, verify_decryption_record
     from electionguard.keyceremony import key_ceremony, verify_backups, verify_commitment_proofs
     from electionguard.remote import RemoteDecryptingTrusteeProxy
     from electionguard.trustee_server import write_trustee_file
@@ -105,16 +105,21 @@ def main():
             proxies.append(RemoteDecryptingTrusteeProxy(g.gid, f"127.0.0.1:{line.split()[1]}", g.x, g.public_key))
         t = time.time()
         dec = Decryption(G, qbar, proxies, [g.gid for g in gk[navail:]], {g.gid: g.public_key for g in gk})
-        counts = dec.decrypt(tally, a.nballots)
+        rec = dec.decrypt_record(tally, a.nballots)
+        counts = rec.counts
         print(f"*** remote decryption ({navail} trustees, {a.nguardians - navail} missing) {time.time() - t:.3f} s")
+        t = time.time()
+        rv = verify_decryption_record(G, qbar, rec, {g.gid: g.public_key for g in gk}, comm)
+        print(f"*** verify decryption record {time.time() - t:.3f} s: {rv}")
         ok = counts == [int(x) for x in expected]
         print(json.dumps({"counts": counts, "expected": [int(x) for x in expected], "match": ok,
+                          "record_checks": rv,
                           "all_took_s": round(time.time() - t_all, 3)}))
         for px in proxies:
             px.finish(ok)
         for p in procs:
             p.wait(timeout=60)
-        return 0 if ok and all_ok else 1
+        return 0 if ok and all_ok and all(rv.values()) else 1
     finally:
         for p in procs:
             if p.poll() is None:
