@@ -1,0 +1,74 @@
+"""Election-record verification: the reference's last workflow step,
+``new Verifier(record, 11).verify()`` (RunRemoteWorkflowTest.java:179-182; the Verifier is
+upstream, electionguard-kotlin-multiplatform-jvm), over the parts of the record the hot
+path produces.  Every exponentiation runs on the GPU through the C ABI:
+
+  * ``guardian_proofs``  Schnorr proofs of every guardian's coefficient commitments
+                         (keyceremony.verify_commitment_proofs);
+  * ``joint_key``        K == prod_i K_i0;
+  * ``ballots``          every disjunctive and contest proof of every ballot (eg_verify_ballots);
+  * ``tally``            the published encrypted tally == the product of the ballots'
+                         ciphertexts per real selection (runAccumulateBallots, :151);
+  * ``decryption.*``     decrypt.verify_decryption_record (share proofs, recovery keys,
+                         quorum, B == M g^t).
+
+Manifest, hash-chain and protobuf-format checks are record plumbing outside the hot path
+ and are not restated.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+from .ballot import ElectionKey, EncryptedBallots, Manifest, Verifier
+from .core.group import GroupContext, as_p_array
+from .decrypt import DecryptionRecord, verify_decryption_record
+from .keyceremony import verify_commitment_proofs
+
+
+@dataclass
+class GuardianRecord:
+    gid: str
+    x: int
+    commitments: List[int]          # K_ij = g^{a_ij}
+    proofs: List[Tuple[int, int]]   # Schnorr (c, v) per commitment
+
+
+@dataclass
+class ElectionRecord:
+    manifest: Manifest
+    qbar: int                       # extended base hash Q-bar
+    joint_key: int                  # K
+    guardians: List[GuardianRecord]
+    ballots: EncryptedBallots
+    encrypted_tally: np.ndarray     # (n_real, 2, 512)
+    decryption: DecryptionRecord
+
+
+def verify_election_record(group: GroupContext, rec: ElectionRecord, window_bits: int = 8) -> Dict[str, bool]:
+    """-> {check name: passed}.  A check that cannot run because an earlier one failed
+    structurally (wrong shapes) reports False."""
+    out: Dict[str, bool] = {}
+    comm = [k for g in rec.guardians for k in g.commitments]
+    prf = [p for g in rec.guardians for p in g.proofs]
+    out["guardian_proofs"] = len(comm) == len(prf) and all(verify_commitment_proofs(group, comm, prf))
+    k0 = as_p_array([g.commitments[0] for g in rec.guardians])
+    K = int.from_bytes(group.prodP_groups(k0, 1, len(rec.guardians))[0].tobytes(), "big")
+    out["joint_key"] = K == rec.joint_key
+    man = rec.manifest
+    key = ElectionKey(group, rec.joint_key, window_bits=window_bits)
+    ok_s, ok_c, tally = Verifier(group, key, rec.qbar, man).verify(rec.ballots)
+    out["ballots"] = bool(ok_s.all() and ok_c.all())
+    et = np.ascontiguousarray(rec.encrypted_tally, dtype=np.uint8).reshape(-1, 2, 512)
+    out["tally"] = et.shape == tally.shape and bool(np.array_equal(et, tally))
+    dtexts = np.ascontiguousarray(rec.decryption.texts, dtype=np.uint8).reshape(-1, 2, 512)
+    same_texts = dtexts.shape == et.shape and bool(np.array_equal(dtexts, et))
+    pks = {g.gid: g.commitments[0] for g in rec.guardians}
+    commitments = {g.gid: g.commitments for g in rec.guardians}
+    dv = verify_decryption_record(group, rec.qbar, rec.decryption, pks, commitments)
+    out["decryption.texts"] = same_texts
+    for name, ok in dv.items():
+        out[f"decryption.{name}"] = ok
+    return out

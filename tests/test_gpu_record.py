@@ -1,0 +1,84 @@
+"""GPU: election-record verification (record.verify_election_record, the reference's
+``Verifier(record, 11).verify()`` step, RunRemoteWorkflowTest.java:179-182): an honest
+5-guardian / quorum-3 record with 2 missing guardians passes every check, and each
+tampering fails the check that covers it (and only the checks that depend on it)."""
+import copy
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def election(group):
+    from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
+    from electionguard.decrypt import DecryptingTrustee, Decryption
+    from electionguard.keyceremony import key_ceremony
+    from electionguard.record import ElectionRecord, GuardianRecord
+    gk, K = key_ceremony(group, 5, 3, seed=77)
+    man = Manifest(2, 3, 1)
+    rng = np.random.default_rng(77)
+    nb = 12
+    votes = random_votes(rng, man, nb)
+    qbar = 0xABCDEF
+    key = ElectionKey(group, K)
+    eb = batch_encryption(group, key, qbar, man, votes, random_scalars(rng, (nb, man.nsel, 4), group.q),
+                          random_scalars(rng, (nb, man.n_contests), group.q))
+    _, _, tally = Verifier(group, key, qbar, man).verify(eb)
+    comm = {g.gid: g.commitments for g in gk}
+    avail = [DecryptingTrustee(group, g, comm) for g in gk[:3]]
+    drec = Decryption(group, qbar, avail, [g.gid for g in gk[3:]], {g.gid: g.public_key for g in gk}) \
+        .decrypt_record(tally, nb)
+    rec = ElectionRecord(man, qbar, K, [GuardianRecord(g.gid, g.x, list(g.commitments), list(g.proofs)) for g in gk],
+                         eb, tally, drec)
+    expected = votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].sum(axis=0).reshape(-1)
+    return rec, [int(x) for x in expected]
+
+
+def test_honest_record_passes(group, election):
+    from electionguard.record import verify_election_record
+    rec, expected = election
+    assert rec.decryption.counts == expected
+    res = verify_election_record(group, rec)
+    assert all(res.values()), res
+
+
+def _failed(res):
+    return sorted(k for k, v in res.items() if not v)
+
+
+def test_tampered_records_fail_their_check(group, election):
+    from electionguard.ballot import EncryptedBallots
+    from electionguard.record import verify_election_record
+    rec, _ = election
+    p = group.p
+
+    bad = copy.copy(rec)
+    g0 = copy.deepcopy(rec.guardians[0])
+    c, v = g0.proofs[1]
+    g0.proofs[1] = (c, (v + 1) % group.q)
+    bad.guardians = [g0] + rec.guardians[1:]
+    assert _failed(verify_election_record(group, bad)) == ["guardian_proofs"]
+
+    bad = copy.copy(rec)
+    bad.joint_key = rec.joint_key * group.g % p
+    # the ballots were encrypted under the real K, so their proofs fail under the wrong one too
+    assert _failed(verify_election_record(group, bad)) == ["ballots", "joint_key"]
+
+    bad = copy.copy(rec)
+    rp = rec.ballots.rproof.copy()
+    rp[5, 2, 1, 7] ^= 0x10
+    bad.ballots = EncryptedBallots(rec.ballots.cts, rp, rec.ballots.cproof)
+    assert _failed(verify_election_record(group, bad)) == ["ballots"]
+
+    bad = copy.copy(rec)
+    et = rec.encrypted_tally.copy()
+    et[[0, 1]] = et[[1, 0]]   # two selections' totals swapped
+    bad.encrypted_tally = et
+    assert _failed(verify_election_record(group, bad)) == ["decryption.texts", "tally"]
+
+    bad = copy.copy(rec)
+    bad.decryption = copy.deepcopy(rec.decryption)
+    bad.decryption.counts[3] += 1
+    assert _failed(verify_election_record(group, bad)) == ["decryption.tally"]
