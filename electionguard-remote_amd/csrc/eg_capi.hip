@@ -124,7 +124,7 @@ struct eg_fixed_base {
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_YA, W_YB, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_YA, W_YB, W_NSLOT
 };
 
 struct eg_ctx {
@@ -147,6 +147,9 @@ struct eg_ctx {
   // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
   // most recently used first
   std::vector<std::pair<std::array<uint8_t, 512>, eg_fixed_base*>> share_keys;
+  // host-pointer verify: uploads of chunk k+1 on their own stream overlap chunk k's kernels
+  hipStream_t copy = nullptr;
+  hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
 };
 static std::vector<ProfRec>& prof_of(eg_ctx* c) { return c->prof; }
 
@@ -474,6 +477,14 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);
+  if (c->copy) {
+    hipStreamSynchronize(c->copy);
+    hipStreamDestroy(c->copy);
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (c->up_ev[i]) hipEventDestroy(c->up_ev[i]);
+    if (c->done_ev[i]) hipEventDestroy(c->done_ev[i]);
+  }
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return EG_OK;

@@ -104,3 +104,24 @@ def test_encrypt_chunk_boundary(group):
     assert np.array_equal(part.cproof, eb.cproof[a:b])
     ok_s, ok_c, _ = Verifier(group, key, qbar, man).verify(eb, with_tally=False)
     assert ok_s.all() and ok_c.all()
+
+
+def test_three_streamed_chunks(group):
+    """eg_verify_ballots streams host input through two upload buffers on a copy stream:
+    with three chunks the third reuses the first buffer set (waits on chunk 0's kernels).
+    Verdicts, the tally and a tamper in the third chunk must all come out exactly."""
+    from electionguard.ballot import EncryptedBallots, Manifest, Verifier
+    man = Manifest(1, 1, 1)
+    nb = 2 * 16384 + 100
+    key, K, qbar, eb = _encrypt(group, man, nb, 61)
+    V = Verifier(group, key, qbar, man)
+    ok_s, ok_c, tally = V.verify(eb)
+    assert ok_s.all() and ok_c.all()
+    assert np.array_equal(tally, _tally_products(man, eb))
+    cts = eb.cts.copy()
+    cts[nb - 7, 1, 0, 100] ^= 0x04   # the placeholder's pad in the third chunk
+    rp = eb.rproof.copy()
+    rp[5, 0, 2, 9] ^= 0x01           # first chunk
+    ok_s, ok_c, _ = V.verify(EncryptedBallots(cts, rp, eb.cproof), with_tally=False)
+    assert np.argwhere(~ok_s).tolist() == [[5, 0], [nb - 7, 1]]
+    assert np.argwhere(~ok_c).tolist() == [[nb - 7, 0]]
