@@ -143,6 +143,8 @@ def main():
     total_ballots = nb * world * a.steps
     # configs[1] = the 4x5 bench default; configs[4] = the 100-selection manifest (20 x 5)
     cfg_name = {(4, 5): "configs[1]", (20, 5): "configs[4] shape"}.get((a.contests, a.selections), "custom manifest")
+    if (a.contests, a.selections) == (4, 5) and nb * world == 1_000_000:
+        cfg_name = f"configs[2] (1M ballots over {world} GPU{'s' if world > 1 else ''})"
     coll = "RCCL" if (dist is None or backend == "nccl") else backend
     value = total_ballots / el
     # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
