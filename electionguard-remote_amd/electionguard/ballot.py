@@ -127,6 +127,19 @@ def batch_encryption(group: GroupContext, key: ElectionKey, qbar: int, man: Mani
     return EncryptedBallots(cts, rp, cp)
 
 
+def batch_encryption_device(group: GroupContext, key: ElectionKey, qbar: int, man: Manifest, nb: int, d_votes: int,
+                            d_sel_nonces: int, d_contest_nonces: int, d_cts: int, d_rproof: int,
+                            d_cproof: int) -> None:
+    """batch_encryption on device pointers (e.g. torch tensors' data_ptr()): the same
+    layouts, inputs and outputs resident in HBM (eg_encrypt_ballots_dev)."""
+    if nb:
+        key.ensure()
+        native.check(group._lib, "eg_encrypt_ballots_dev",
+                     group._lib.eg_encrypt_ballots_dev(group.handle, native.buf(q_bytes(qbar)), nb, man.n_contests,
+                                                       man.spc, d_votes, d_sel_nonces, d_contest_nonces, d_cts,
+                                                       d_rproof, d_cproof))
+
+
 class Verifier:
     """Ballot-proof verification + homomorphic tally (Verifier.verify / runAccumulateBallots)."""
 

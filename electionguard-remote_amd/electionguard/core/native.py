@@ -22,7 +22,7 @@ EXPORTED = [
     "eg_fixed_base_create", "eg_fixed_base_destroy", "eg_powp_batch", "eg_fb_pow_batch",
     "eg_powp_batch_dev", "eg_fb_pow_batch_dev",
     "eg_multp_batch", "eg_prod_reduce", "eg_multinv_batch", "eg_verify_ballots",
-    "eg_set_election_key", "eg_verify_ballots_dev", "eg_encrypt_ballots",
+    "eg_set_election_key", "eg_verify_ballots_dev", "eg_encrypt_ballots", "eg_encrypt_ballots_dev",
     "eg_trustee_decrypt_batch", "eg_verify_shares",
 ]
 
@@ -72,6 +72,7 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_set_election_key": ([P, P, I], I),
         "eg_verify_ballots_dev": ([P, P, S, S, S, S, U32, P, P, P, P, P, P], I),
         "eg_encrypt_ballots": ([P, P, S, S, S, P, P, P, P, P, P], I),
+        "eg_encrypt_ballots_dev": ([P, P, S, S, S, P, P, P, P, P, P], I),
         "eg_trustee_decrypt_batch": ([P, P, P, P, P, S, P, P], I),
         "eg_verify_shares": ([P, P, P, P, P, P, S, P], I),
     }

@@ -139,6 +139,13 @@ int eg_encrypt_ballots(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nb
                        size_t ncontest, size_t spc, const uint8_t* votes,
                        const uint8_t* sel_nonces, const uint8_t* contest_nonces,
                        uint8_t* cts, uint8_t* rproof, uint8_t* cproof);
+/* Same, device pointers (inputs and outputs resident in HBM); returns when the outputs
+ * are written.  The votes (1 byte per selection) are read back to the host to build the
+ * job tables; nonces and outputs never leave the device. */
+int eg_encrypt_ballots_dev(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nballots,
+                           size_t ncontest, size_t spc, const uint8_t* d_votes,
+                           const uint8_t* d_sel_nonces, const uint8_t* d_contest_nonces,
+                           uint8_t* d_cts, uint8_t* d_rproof, uint8_t* d_cproof);
 
 /* ---- trustee partial decryption (DecryptingTrusteeIF) ----
  * directDecrypt (RunRemoteDecryptingTrustee.java:189-193): per text i,

@@ -125,3 +125,32 @@ def test_three_streamed_chunks(group):
     ok_s, ok_c, _ = V.verify(EncryptedBallots(cts, rp, eb.cproof), with_tally=False)
     assert np.argwhere(~ok_s).tolist() == [[5, 0], [nb - 7, 1]]
     assert np.argwhere(~ok_c).tolist() == [[nb - 7, 0]]
+
+
+def test_device_encryption_matches_host(group):
+    """eg_encrypt_ballots_dev (inputs and outputs in HBM, two chunks) writes exactly the
+    bytes of the host-pointer eg_encrypt_ballots for the same injected nonces."""
+    import torch
+    from electionguard.ballot import (ElectionKey, Manifest, batch_encryption, batch_encryption_device,
+                                      random_scalars, random_votes)
+    from electionguard.keyceremony import key_ceremony
+    man = Manifest(1, 2, 1)
+    nb = 16384 + 9
+    _, K = key_ceremony(group, 3, 3, seed=71)
+    key = ElectionKey(group, K, window_bits=12)
+    rng = np.random.default_rng(71)
+    votes = random_votes(rng, man, nb)
+    sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
+    cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    eb = batch_encryption(group, key, 555, man, votes, sn, cn)
+    d = torch.device("cuda", 0)
+    dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(d) for x in (votes, sn, cn))
+    oc = torch.empty(eb.cts.shape, dtype=torch.uint8, device=d)
+    orp = torch.empty(eb.rproof.shape, dtype=torch.uint8, device=d)
+    ocp = torch.empty(eb.cproof.shape, dtype=torch.uint8, device=d)
+    torch.cuda.synchronize()
+    batch_encryption_device(group, key, 555, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(), oc.data_ptr(),
+                            orp.data_ptr(), ocp.data_ptr())
+    assert np.array_equal(oc.cpu().numpy(), eb.cts)
+    assert np.array_equal(orp.cpu().numpy(), eb.rproof)
+    assert np.array_equal(ocp.cpu().numpy(), eb.cproof)
