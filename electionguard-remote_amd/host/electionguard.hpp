@@ -633,6 +633,16 @@ inline ElementModQ lagrangeCoefficient(const GroupContext& G, const std::vector<
   return G.mulQ(num, G.invQ(den));
 }
 
+// What the mediator publishes for a decrypted tally (the share data the reference's
+// Verifier(record, 11).verify() re-checks, RunRemoteWorkflowTest.java:179-182).
+struct DecryptionRecord {
+  std::vector<ElGamalCiphertext> texts;                                  // encrypted tally
+  std::map<std::string, int> xs;                                         // available guardian -> x
+  std::map<std::string, std::vector<DirectDecryptionAndProof>> direct;   // available -> n shares
+  std::map<std::string, std::map<std::string, std::vector<CompensatedDecryptionAndProof>>> compensated;  // missing -> available -> n
+  std::vector<std::optional<int64_t>> counts;
+};
+
 // Mediator combine: new Decryption(group, init, trustees, missing).decrypt(tally)
 // (RunRemoteDecryptor.java:261-262): verify every share's proof, Lagrange-weight the
 // compensated shares, M = prod M_i, T = data / M, t = dLogG(T).
@@ -643,9 +653,19 @@ class Decryption {
       : G_(G), qbar_(qbar), trustees_(std::move(trustees)), missing_(std::move(missing)) {}
 
   std::vector<std::optional<int64_t>> decrypt(const std::vector<ElGamalCiphertext>& tally, int64_t maxCount) {
+    return decryptRecord(tally, maxCount).counts;
+  }
+
+  // decrypt() keeping every share and proof (the published decryption record)
+  DecryptionRecord decryptRecord(const std::vector<ElGamalCiphertext>& tally, int64_t maxCount) {
     const size_t n = tally.size();
+    DecryptionRecord rec;
+    rec.texts = tally;
     std::vector<int> xs;
-    for (auto* t : trustees_) xs.push_back(t->xCoordinate());
+    for (auto* t : trustees_) {
+      xs.push_back(t->xCoordinate());
+      rec.xs[t->id()] = t->xCoordinate();
+    }
     std::vector<std::vector<ElementModP>> parts;
     for (auto* tr : trustees_) {
       auto res = tr->directDecrypt(G_, tally, qbar_, nullptr);
@@ -659,6 +679,7 @@ class Decryption {
       const auto ok = verifyShares(G_, qbar_, std::vector<ElementModP>(n, tr->electionPublicKey()), tally, M, pr);
       if (std::find(ok.begin(), ok.end(), false) != ok.end())
         throw ArithmeticException("invalid direct decryption proof from " + tr->id());
+      rec.direct[tr->id()] = res;
       parts.push_back(std::move(M));
     }
     for (const auto& l : missing_)
@@ -675,6 +696,7 @@ class Decryption {
         const auto ok = verifyShares(G_, qbar_, rk, tally, M, pr);
         if (std::find(ok.begin(), ok.end(), false) != ok.end())
           throw ArithmeticException("invalid compensated decryption proof from " + tr->id() + " for " + l);
+        rec.compensated[l][tr->id()] = res;
         const ElementModQ w = lagrangeCoefficient(G_, xs, tr->xCoordinate());
         parts.push_back(G_.powPBatch(M, std::vector<ElementModQ>(n, w)));
       }
@@ -687,7 +709,8 @@ class Decryption {
     std::vector<ElementModP> data;
     for (const auto& t : tally) data.push_back(t.data);
     const auto T = G_.multPBatch(data, G_.multInvBatch(M));
-    return G_.dLogGBatch(T, maxCount);
+    rec.counts = G_.dLogGBatch(T, maxCount);
+    return rec;
   }
 
  private:
@@ -696,6 +719,79 @@ class Decryption {
   std::vector<DecryptingTrusteeIF*> trustees_;
   std::vector<std::string> missing_;
 };
+
+// Record-level checks of a tally decryption, independent of the mediator that made it (the
+// decryption part of Verifier(record, 11).verify(), RunRemoteWorkflowTest.java:179-182);
+// same checks as the Python decrypt.verify_decryption_record, every exponentiation on the GPU.
+struct DecryptionRecordChecks {
+  bool directProofs = true, recoveryKeys = true, compensatedProofs = true, quorum = true, tally = true;
+  bool all() const { return directProofs && recoveryKeys && compensatedProofs && quorum && tally; }
+};
+
+inline DecryptionRecordChecks verifyDecryptionRecord(const GroupContext& G, const ElementModQ& qbar,
+                                                     const DecryptionRecord& rec,
+                                                     const std::map<std::string, ElementModP>& publicKeys,
+                                                     const std::map<std::string, std::vector<ElementModP>>& commitments) {
+  DecryptionRecordChecks out;
+  const size_t n = rec.texts.size();
+  auto allTrue = [](const std::vector<bool>& v) { return std::find(v.begin(), v.end(), false) == v.end(); };
+  for (const auto& [gid, res] : rec.direct) {
+    if (res.size() != n) { out.directProofs = false; continue; }
+    std::vector<ElementModP> M;
+    std::vector<GenericChaumPedersenProof> pr;
+    for (const auto& r : res) { M.push_back(r.partialDecryption); pr.push_back(r.proof); }
+    out.directProofs &= allTrue(verifyShares(G, qbar, std::vector<ElementModP>(n, publicKeys.at(gid)), rec.texts, M, pr));
+  }
+  if (rec.counts.size() != n) out.tally = false;
+  for (const auto& c : rec.counts) out.tally &= c.has_value();
+  for (const auto& [l, byAvail] : rec.compensated) {
+    out.quorum &= byAvail.size() == rec.direct.size();
+    for (const auto& [gid, res] : byAvail) {
+      out.quorum &= rec.direct.count(gid) == 1;
+      if (res.size() != n) { out.compensatedProofs = out.recoveryKeys = false; continue; }
+      // g^{P_l(x_i)} = prod_j K_{l,j}^{x_i^j}
+      const auto& comm = commitments.at(l);
+      std::vector<ElementModQ> e;
+      ElementModQ xj = G.uIntToElementModQ(1);
+      const ElementModQ x = G.uIntToElementModQ((uint64_t)rec.xs.at(gid));
+      for (size_t j = 0; j < comm.size(); ++j) { e.push_back(xj); xj = G.mulQ(xj, x); }
+      const ElementModP want = G.multP(G.powPBatch(comm, e));
+      std::vector<ElementModP> M, rk;
+      std::vector<GenericChaumPedersenProof> pr;
+      for (const auto& r : res) {
+        out.recoveryKeys &= r.recoveredPublicKeyShare == want;
+        M.push_back(r.partialDecryption); pr.push_back(r.proof); rk.push_back(r.recoveredPublicKeyShare);
+      }
+      out.compensatedProofs &= allTrue(verifyShares(G, qbar, rk, rec.texts, M, pr));
+    }
+  }
+  if (!out.quorum || !out.tally || n == 0) return out;
+  // B == M g^t with M = prod_i M_i * prod_l prod_i M_{l,i}^{w_i}
+  std::vector<int> xs;
+  for (const auto& [gid, x] : rec.xs) xs.push_back(x);
+  std::vector<std::vector<ElementModP>> parts;
+  for (const auto& [gid, res] : rec.direct) {
+    std::vector<ElementModP> M;
+    for (const auto& r : res) M.push_back(r.partialDecryption);
+    parts.push_back(std::move(M));
+  }
+  for (const auto& [l, byAvail] : rec.compensated)
+    for (const auto& [gid, res] : byAvail) {
+      std::vector<ElementModP> M;
+      for (const auto& r : res) M.push_back(r.partialDecryption);
+      parts.push_back(G.powPBatch(M, std::vector<ElementModQ>(n, lagrangeCoefficient(G, xs, rec.xs.at(gid)))));
+    }
+  const size_t k = parts.size();
+  std::vector<ElementModP> stacked;
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < k; ++j) stacked.push_back(parts[j][i]);
+  const auto M = G.prodPGroups(stacked, n, k);
+  std::vector<ElementModQ> t;
+  for (const auto& c : rec.counts) t.push_back(G.uIntToElementModQ((uint64_t)*c));
+  const auto lhs = G.multPBatch(M, G.gPowPBatch(t));
+  for (size_t i = 0; i < n; ++i) out.tally &= lhs[i] == rec.texts[i].data;
+  return out;
+}
 
 // ---------------------------------------------------------------- ballots (B1 batch users)
 struct Manifest {  // synthetic manifest shape (RandomBallotProvider, RunRemoteWorkflowTest.java:133)

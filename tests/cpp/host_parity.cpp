@@ -238,6 +238,20 @@ static int run_gpu(const char* path) {
     Decryption dec(G, qb, ptrs, {"guardian4", "guardian5"});
     const auto got = dec.decrypt(tally, 1000);
     for (size_t i = 0; i < n; ++i) EXPECT(got[i] && *got[i] == counts[i], "decrypted count #" << i);
+    // the published decryption record verifies; tampering fails exactly the covering check
+    const DecryptionRecord rec = dec.decryptRecord(tally, 1000);
+    std::map<std::string, ElementModP> pks;
+    for (const auto& g : gs) pks[g.id] = g.publicKey();
+    EXPECT(verifyDecryptionRecord(G, qb, rec, pks, comm).all(), "decryption record verifies");
+    DecryptionRecord bad = rec;
+    bad.counts[3] = *bad.counts[3] + 1;
+    auto chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.tally && chk.directProofs && chk.compensatedProofs && chk.recoveryKeys, "tampered count flagged");
+    bad = rec;
+    auto& rk = bad.compensated["guardian4"]["guardian2"][5].recoveredPublicKeyShare;
+    rk = G.multPBatch({rk}, {G.gPowP(G.uIntToElementModQ(1))})[0];
+    chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.recoveryKeys && !chk.compensatedProofs && chk.tally && chk.directProofs, "tampered recovery key flagged");
     // dLogG above the bound -> not found
     EXPECT(!G.dLogG(G.gPowP(G.uIntToElementModQ(1500)), 1000).has_value(), "dLogG beyond maxResult");
   }
