@@ -109,3 +109,40 @@ def test_oracle_schnorr_and_backup_checks():
     share = O.poly_eval(gs[2].coeffs, gs[0].x, G.q)
     assert O.verify_backup_share(G, share, gs[2], gs[0].x)
     assert not O.verify_backup_share(G, share, gs[2], gs[1].x)
+
+
+def test_oracle_threshold_decryption_round_trip():
+    """The oracle's own threshold decryption (the checker the GPU trustee / record tests lean
+    on): 4 guardians, quorum 2, guardians 2 and 4 missing.  Every share proof verifies,
+    recovery keys match the compensating guardian's share, and combine() recovers the
+    encrypted counts; a tampered share breaks its proof."""
+    import random
+
+    import eg_oracle as O
+    G = O.production_group()
+    rng = random.Random(5)
+    gs, K = O.key_ceremony(G, 4, 2, rng)
+    avail, missing = [gs[0], gs[2]], [gs[1], gs[3]]
+    counts = [0, 3, 17]
+    texts = [O.encrypt(G, K, m, rng.randrange(1, G.q)) for m in counts]
+    qbar = rng.randrange(G.q)
+    direct, comp = {}, {}
+    for gd in avail:
+        res = O.direct_decrypt(G, qbar, gd, texts, [rng.randrange(1, G.q) for _ in texts])
+        assert all(O.verify_share(G, qbar, gd.K, t, M, pr) for t, (M, pr) in zip(texts, res))
+        direct[gd.gid] = [M for M, _ in res]
+    for gl in missing:
+        comp[gl.gid] = {}
+        for gd in avail:
+            res = O.compensated_decrypt(G, qbar, gd, gl, texts, [rng.randrange(1, G.q) for _ in texts])
+            for t, (M, pr, rk) in zip(texts, res):
+                assert rk == G.gPowP(O.poly_eval(gl.coeffs, gd.x, G.q))
+                assert O.verify_share(G, qbar, rk, t, M, pr)
+            comp[gl.gid][gd.gid] = [M for M, _, _ in res]
+    xs = {g.gid: g.x for g in avail}
+    for i, t in enumerate(texts):
+        got = O.combine(G, t, {g: v[i] for g, v in direct.items()},
+                        {l: {g: v[i] for g, v in by.items()} for l, by in comp.items()}, xs, 20)
+        assert got == counts[i]
+    M, pr = O.direct_decrypt(G, qbar, avail[0], texts[:1], [7])[0]
+    assert not O.verify_share(G, qbar, avail[0].K, texts[0], M * G.g % G.p, pr)
