@@ -306,6 +306,9 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
     avail = list(rec.direct)
     for gid in avail:
         res = rec.direct[gid]
+        if gid not in public_keys or gid not in rec.xs:
+            out["direct_proofs"] = out["quorum"] = False
+            continue
         out["direct_proofs"] &= len(res) == n and bool(
             verify_shares(G, qbar, [public_keys[gid]] * n, T, [r.partialDecryption for r in res],
                           [r.proof for r in res]).all())
@@ -313,8 +316,14 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
         out["tally"] = False
     for l, by_avail in rec.compensated.items():
         out["quorum"] &= sorted(by_avail) == sorted(avail)
-        comm = commitments[l]
+        comm = commitments.get(l)
+        if comm is None:  # a "missing guardian" the key ceremony never had
+            out["recovery_keys"] = out["compensated_proofs"] = False
+            continue
         for gid, res in by_avail.items():
+            if gid not in rec.xs:
+                out["quorum"] = False
+                continue
             x = rec.xs[gid]
             exps = [pow(x, j, G.q) for j in range(len(comm))]
             want = _be_int(G.prodP_groups(G.powP_batch(comm, exps), 1, len(comm))[0])
@@ -322,6 +331,10 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
             out["compensated_proofs"] &= len(res) == n and bool(
                 verify_shares(G, qbar, [r.recoveredPublicKeyShare for r in res], T,
                               [r.partialDecryption for r in res], [r.proof for r in res]).all())
+    lengths_ok = all(len(rec.direct[g]) == n for g in avail) and all(
+        len(res) == n for by in rec.compensated.values() for res in by.values())
+    if not lengths_ok:
+        out["tally"] = False
     if not (out["quorum"] and out["tally"] and n):
         return out
     xs = [rec.xs[g] for g in avail]
