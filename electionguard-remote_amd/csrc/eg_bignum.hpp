@@ -64,6 +64,10 @@ struct MontConsts {
   uint32_t n0;         // -p^-1 mod 2^kLimbBits
   uint32_t friendly;   // n0 == 1 (p = -1 mod 2^kLimbBits): EG production group
   uint32_t mask;       // 2^kLimbBits - 1 (read at run time so AND can fuse into DPP moves)
+  // Subgroup (residue) test x^q == 1, evaluated as x^(2^256) == x^c with c = 2^256 - q
+  // (x != 0): c is public, 189 for the EG q = 2^256 - 189 (8 bits, 7 sq + 5 mul).
+  uint32_t qc[8];      // c = 2^256 - q, little-endian words
+  uint32_t qc_bits;    // bit length of c
 };
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

@@ -125,7 +125,7 @@ struct eg_fixed_base {
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_YA, W_YB, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_YA, W_YB, W_RZ, W_RC, W_CRF, W_NSLOT
 };
 
 struct eg_ctx {
@@ -200,7 +200,7 @@ static int launch_export(eg_ctx* c, const uint32_t* d_in, size_t n, uint8_t* d_b
 struct MMCount {
   double mul = 0, sqr = 0;
 };
-static MMCount pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
+static MMCount pow_job_mm(const MontConsts& H, const PowShape& S, const FbTab& f0, const FbTab& f1) {
   MMCount n;
   if (S.has_base) {
     if (S.comb) {
@@ -209,6 +209,12 @@ static MMCount pow_job_mm(const PowShape& S, const FbTab& f0, const FbTab& f1) {
       else
         n.sqr += (double)((kCombH - 1) * kCombW);
       n.mul += (double)((1 << kCombH) - kCombH - 1);
+      if (S.resid && !S.gather && H.qc_bits) {  // z: 48 squarings past y_4; w = B^c ladder
+        int pop = 0;
+        for (int w = 0; w < 8; ++w) pop += __builtin_popcount(H.qc[w]);
+        n.sqr += (double)(256 - (kCombH - 1) * kCombW) + (double)(H.qc_bits - 1);
+        n.mul += (double)(pop - 1);
+      }
     } else {
       n.mul += 14.0;
     }
@@ -252,7 +258,8 @@ static size_t pow_scratch_per_group(const PowShape& S) {
 }
 static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
                       const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1, uint32_t* yout = nullptr,
-                      const uint32_t* ygat = nullptr, const PowTail* tail = nullptr) {
+                      const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr) {
+  if (S.resid && (!S.comb || S.gather || !rout)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
   if (tail && tail->S.gather && (!tail->S.comb || !tail->ygat))
     return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
@@ -262,8 +269,8 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   const size_t per1 = tail ? pow_scratch_per_group(tail->S) : 0;
   // bound the per-launch scratch (table of 16/32 powers per job)
   const size_t max_jobs = (size_t)1 << 18;
-  const MMCount mm_job = pow_job_mm(S, f0, f1);
-  const MMCount mm_tail = tail ? pow_job_mm(tail->S, f0, f1) : MMCount{};
+  const MMCount mm_job = pow_job_mm(c->h, S, f0, f1);
+  const MMCount mm_tail = tail ? pow_job_mm(c->h, tail->S, f0, f1) : MMCount{};
   size_t off = 0;
   do {
     const size_t nj = std::min(max_jobs, njobs - off);
@@ -273,11 +280,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
     if (rc) return rc;
     PowPart P0{S, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
-               yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat};
+               yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat, rout ? rout + off * 2 * kW : nullptr};
     PowPart P1{};
     if (nt) {
       P1 = PowPart{tail->S, tail->jobs, (uint32_t)nt, grid_for(nt),
-                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat};
+                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, nullptr};
     }
     ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
@@ -432,6 +439,18 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   c->h.n0 = (0u - inv) & kMask;
   c->h.friendly = c->h.n0 == 1 ? 1u : 0u;
   c->h.mask = kMask;
+  {  // c = 2^256 - q (mod 2^256) for the residue test x^(2^256) == x^c
+    const Big q = be_to_words(q_be, 32);
+    int64_t br = 0;
+    for (int i = 0; i < 8; ++i) {
+      br += -(int64_t)q[i];
+      c->h.qc[i] = (uint32_t)br;
+      br >>= 32;
+    }
+    c->h.qc_bits = 0;
+    for (int b = 255; b >= 0; --b)
+      if ((c->h.qc[b >> 5] >> (b & 31)) & 1u) { c->h.qc_bits = (uint32_t)b + 1; break; }
+  }
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {

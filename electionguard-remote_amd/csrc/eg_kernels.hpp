@@ -154,8 +154,7 @@ __global__ void __launch_bounds__(kBlock) k_import(const MontConsts* __restrict_
 
 // Fully normalise a value held in the group slot (limbs in device format, value <= p)
 // by group-lane 0; maps p -> 0.  Then write 512 big-endian bytes.
-__device__ __forceinline__ void slot_to_be(const MontConsts* __restrict__ C, uint32_t* slot,
-                                           uint8_t* __restrict__ dst, bool do_store) {
+__device__ __forceinline__ void slot_normalize(const MontConsts* __restrict__ C, uint32_t* slot) {
   if (glane() == 0) {
     uint32_t carry = 0;
     bool eq = true;
@@ -172,6 +171,11 @@ __device__ __forceinline__ void slot_to_be(const MontConsts* __restrict__ C, uin
     }
   }
   wave_sync();
+}
+
+__device__ __forceinline__ void slot_to_be(const MontConsts* __restrict__ C, uint32_t* slot,
+                                           uint8_t* __restrict__ dst, bool do_store) {
+  slot_normalize(C, slot);
   constexpr int kPer = 128 / kT;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -206,6 +210,50 @@ __global__ void __launch_bounds__(kBlock) k_export(const MontConsts* __restrict_
   regs_to_lds(slot, x);
   wave_sync();
   slot_to_be(C, slot, be + (size_t)gid * 512, gid < n);
+}
+
+// Residue (subgroup) test of n bases from their k_pow residue pairs (PowShape::resid):
+//   pair i = (z, w) = (B^(2^256), B^c) in Montgomery form;  B^q == 1  <=>  z == w and B != 0
+// (B^(2^256) = B^q * B^c, and B is invertible unless B == 0, where z = w = 0).
+// flags[i * fstride] &= verdict — the per-element range flag of the verifier (k_import).
+// Cost: 2 MM (leaving the Montgomery domain) + two serial normalisations per base.
+template <bool F>
+__global__ void __launch_bounds__(kBlock) k_resid_check(const MontConsts* __restrict__ C,
+                                                        const uint32_t* __restrict__ pairs, uint32_t n,
+                                                        uint8_t* __restrict__ flags, uint32_t fstride) {
+  const uint32_t gid = group_id();
+  const uint32_t e = gid < n ? gid : n - 1;
+  uint32_t* slot = group_slot();
+  Mont<F> M;
+  M.load(C);
+  uint32_t z[kL], x[kL];
+  bool eq = true, nz = false;
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    load_elem(x, pairs + ((size_t)e * 2 + h) * kW);
+    elem_to_lds(slot, C->unit);
+    wave_sync();
+    M.mul(x, slot);  // value in [0, p]
+    wave_sync();
+    regs_to_lds(slot, x);
+    wave_sync();
+    slot_normalize(C, slot);  // canonical limbs, p -> 0
+    const uint32_t* s = slot + glane() * kLP;
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < kL; ++j) { z[j] = s[j]; nz |= z[j] != 0; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kL; ++j) eq &= z[j] == s[j];
+    }
+    wave_sync();
+  }
+  const uint64_t neq = __ballot(!eq), nzb = __ballot(nz);
+  const uint64_t gmask = (uint64_t)((1u << kT) - 1u) << (gslot() * kT);
+  if (glane() == 0 && gid < n) {
+    const bool ok = (neq & gmask) == 0 && (nzb & gmask) != 0;
+    if (!ok) flags[(size_t)gid * fstride] = 0;
+  }
 }
 
 // out[i*so] = a[i*sa] * b[i*sb]  (Montgomery form; strides in elements)
@@ -244,6 +292,9 @@ struct PowShape {
   uint32_t gather;     // comb jobs whose base is a PRODUCT of `gather` earlier comb bases (the contest
                        // aggregates A = prod alpha, B = prod beta): y_k = prod of their y_k (ygat,
                        // job J[2] onwards) instead of 208 squarings; 0 = none
+  uint32_t resid;      // comb jobs (not gather): also write the residue-test pair of the base B,
+                       // z = B^(2^256) (48 squarings past y_4) and w = B^c, c = 2^256 - q, to
+                       // rout[2 gid], rout[2 gid + 1]; B^q == 1 iff z == w and B != 0 (k_resid_check)
 };
 
 // Lim-Lee comb parameters for 256-bit exponents: 5 rows of 52 bits.
@@ -290,6 +341,7 @@ struct PowPart {
   uint32_t* scratch;  // per-group table (comb: 32 elements, window: 16)
   uint32_t* yout;     // comb y_1..y_4 per job (optional)
   const uint32_t* ygat;  // gather source (S.gather > 0)
+  uint32_t* rout;        // residue-test pairs (S.resid), 2 device elements per job
 };
 
 template <bool F>
@@ -329,7 +381,11 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   //                y_1..y_4 of every job for a later gather launch
   //   gather     : B = prod of S.gather comb bases whose y_k are in ygat (jobs J[2] ..):
   //                y_k = prod of theirs, 4 x (gather-1) MM instead of 208 squarings
-  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3, kPre = 4, kCTab = 5, kComb = 6, kGather = 7 };
+  //   resid      : after y_4, 48 more squarings give z = B^(2^256); then w = B^c by a public
+  //                left-to-right binary ladder over c = 2^256 - q (C->qc); both to rout
+  uint32_t* __restrict__ rout = P.rout;
+  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3, kPre = 4, kCTab = 5, kComb = 6, kGather = 7,
+               kRsq = 8, kRc = 9 };
   int phase = kBegin, k = 2, w = 0, sub = 0;
   uint32_t o = 0, t = 0, kf = 0;
   bool x_is_one = true;
@@ -355,8 +411,31 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     while (true) {
       if (phase == kPre) {  // k squarings done so far
         if (k < (kCombH - 1) * kCombW) break;  // square
+        if (S.resid) { phase = kRsq; continue; }
         phase = kCTab;
         k = 3;
+        continue;
+      }
+      if (phase == kRsq) {  // z = B^(2^256): squarings 208..255 continue from y_4
+        if (k < 256) break;  // square
+        if (gid < njobs) store_elem(rout + (size_t)gid * 2 * kW, x);
+        load_elem(x, tbl + kW);  // B
+        w = (int)C->qc_bits - 2;
+        sub = 0;
+        phase = kRc;
+        continue;
+      }
+      if (phase == kRc) {  // w = B^c, bits qc_bits-2 .. 0 of the public c
+        if (w < 0) {
+          if (gid < njobs) store_elem(rout + ((size_t)gid * 2 + 1) * kW, x);
+          phase = kCTab;
+          k = 3;
+          continue;
+        }
+        if (sub == 0) break;  // square
+        if ((C->qc[w >> 5] >> (w & 31)) & 1u) { ysrc = tbl + kW; break; }
+        sub = 0;
+        --w;
         continue;
       }
       if (phase == kGather) {  // y_k = prod_i y_k(base i), i = J[2] .. J[2] + gather - 1
@@ -468,6 +547,8 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       }
     }
     else if (phase == kGather) { ++sub; }
+    else if (phase == kRsq) { ++k; }
+    else if (phase == kRc) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
     else if (phase == kCTab) { store_elem(tbl + (size_t)k * kW, x); ++k; }
     else if (phase == kComb) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
     else { ++kf; }

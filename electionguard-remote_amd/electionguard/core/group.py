@@ -20,7 +20,7 @@ from typing import Iterable, List, Optional, Sequence, Union
 import numpy as np
 
 from . import native
-from .constants import G as _G, P as _P, Q as _Q, P_BYTES, Q_BYTES
+from .constants import P_BYTES, Q_BYTES, ProductionMode, constants_for
 
 BytesLike = Union[bytes, bytearray, memoryview]
 
@@ -84,6 +84,7 @@ class GroupContext:
         self.p, self.q, self.g = p, q, g
         self.r = (p - 1) // q if q and (p - 1) % q == 0 else None
         self.device = device
+        self.mode = None  # ProductionMode name when made by productionGroup
         self._lib = native.load()
         self._p_be, self._q_be, self._g_be = p_bytes(p), q_bytes(q), p_bytes(g)
         h = ctypes.c_void_p()
@@ -328,12 +329,15 @@ _PRODUCTION: dict = {}
 _PRODUCTION_LOCK = threading.Lock()
 
 
-def productionGroup(device: int = 0) -> GroupContext:
-    """``KUtils.productionGroup()`` (KUtils.java:10-12): the EG 1.0 4096-bit group, one
-    context per device even when first requested from several threads at once."""
+def productionGroup(device: int = 0, mode: str = ProductionMode.Mode4096) -> GroupContext:
+    """``KUtils.productionGroup()`` (KUtils.java:10-12): ``Mode4096`` is the EG 1.0 4096-bit group
+    the reference's upstream 1.0-SNAPSHOT uses; ``ProductionMode.Mode4096_V2`` selects the EG 2.0
+    group.  One context per (mode, device), even when first requested from several threads."""
     with _PRODUCTION_LOCK:
-        g = _PRODUCTION.get(device)
+        g = _PRODUCTION.get((mode, device))
         if g is None:
-            g = GroupContext(_P, _Q, _G, device=device)
-            _PRODUCTION[device] = g
+            C = constants_for(mode)
+            g = GroupContext(C.p, C.q, C.g, device=device)
+            g.mode = mode
+            _PRODUCTION[(mode, device)] = g
         return g

@@ -215,6 +215,10 @@ struct ModQ {
 // ---------------------------------------------------------------- elements
 class GroupContext;
 
+// Upstream ProductionMode (KUtils.java:5,11): Mode4096 = EG 1.0 (the reference's group);
+// Mode4096_V2 = the EG 2.0 group, a named option (eg_constants.hpp).
+enum class ProductionMode { Mode4096 = 0, Mode4096_V2 = 1 };
+
 // ElementModP: 512-byte big-endian value (common.proto:6-10), unchecked on import.
 struct ElementModP {
   std::array<uint8_t, EG_P_BYTES> be{};
@@ -295,15 +299,19 @@ class GroupContext {
   GroupContext(const GroupContext&) = delete;
   GroupContext& operator=(const GroupContext&) = delete;
 
-  // KUtils.productionGroup() (KUtils.java:10-12): the EG 1.0 4096-bit group, one per device.
-  static GroupContext& productionGroup(int device = 0) {
+  // KUtils.productionGroup() (KUtils.java:10-12): Mode4096 is the EG 1.0 4096-bit group of the
+  // reference's upstream; Mode4096_V2 the EG 2.0 group.  One context per (mode, device).
+  static GroupContext& productionGroup(int device = 0, ProductionMode mode = ProductionMode::Mode4096) {
     static std::mutex mu;
-    static std::map<int, std::unique_ptr<GroupContext>> groups;
+    static std::map<std::pair<int, int>, std::unique_ptr<GroupContext>> groups;
     std::lock_guard<std::mutex> lk(mu);
-    auto& slot = groups[device];
-    if (!slot)
-      slot.reset(new GroupContext(ElementModP::from_hex(constants::kP_HEX), ElementModQ::from_hex(constants::kQ_HEX),
-                                  ElementModP::from_hex(constants::kG_HEX), device));
+    auto& slot = groups[{(int)mode, device}];
+    if (!slot) {
+      const bool v2 = mode == ProductionMode::Mode4096_V2;
+      slot.reset(new GroupContext(ElementModP::from_hex(v2 ? constants::kP_HEX_V2 : constants::kP_HEX),
+                                  ElementModQ::from_hex(v2 ? constants::kQ_HEX_V2 : constants::kQ_HEX),
+                                  ElementModP::from_hex(v2 ? constants::kG_HEX_V2 : constants::kG_HEX), device));
+    }
     return *slot;
   }
 

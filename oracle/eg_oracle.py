@@ -18,8 +18,12 @@ only asserts a protobuf builder is non-null).  What IS pinned:
   mod p, so equality with ``java.math.BigInteger.modPow`` is a mathematical fact;
   this module computes them with CPython ``int`` and is cross-checked against an
   independent OpenSSL-BN restatement (``oracle/eg_oracle_c.c``);
-* the EG 1.0 group constants are re-derived from the spec construction and
-  self-checked (see :func:`derive_production_group`);
+* the group: upstream 1.0-SNAPSHOT (2022) implements ElectionGuard 1.0, whose
+  ``Mode4096`` group is built from Euler's gamma.  :func:`derive_group` re-derives it
+  from gamma and the published delta, and the result is pinned twice: q | p - 1 (2^-256
+  chance for a wrong delta) and g = 2^r mod p reproducing the published EG 1.0
+  generator's leading digits.  The EG 2.0 (ln 2) group is a named second option
+  (``Mode4096_V2``); every golden fixture exists for both;
 * protocol-level restatements (ElGamal, Chaum-Pedersen, tally, threshold
   decryption) follow the ElectionGuard 1.0 spec (cited by the reference at
   src/main/proto/keyceremony_trustee_rpc.proto:40) and the reference's wire
@@ -46,38 +50,58 @@ from typing import Dict, List, Optional, Sequence, Tuple
 # --------------------------------------------------------------------------------------
 
 Q = 2**256 - 189
-# The low-order correction term of the EG 1.0 prime: p's middle 3584 bits are
-# floor(2^3584 * ln 2) + DELTA.  Pinned by q | p - 1 (2^-256 false-positive rate).
-DELTA = int(
-    "25f2da6646e943db028bd17d654a5fe9dc13e777f86b494195b2a55ba0d6d33e6d9d4f", 16)
+# The two 4096-bit groups (electionguard-remote_amd/electionguard/core/constants.py):
+#   Mode4096    -- ElectionGuard 1.0, the group of the reference's upstream 1.0-SNAPSHOT
+#                  (build.gradle.kts:26,55; 2022):
+#                  p = 2^4096 - 2^3840 + 2^256 (floor(2^3584 gamma) + DELTA) - 1
+#   Mode4096_V2 -- ElectionGuard 2.0 (ln 2 in place of Euler's gamma), a named option:
+#                  p = 2^4096 - 2^3840 + 2^256 (floor(2^3584 ln 2) + DELTA') + 2^256 - 1
+# In both, r = (p-1)/q and g = 2^r mod p.  DELTA is the published EG 1.0 correction term;
+# q | p - 1 pins it (a wrong value passes with probability 2^-256), and the derived g must
+# reproduce the published EG 1.0 generator's leading digits 037DE384F98F6E03...
+# DELTA' is the first delta of its residue class with p and (p-1)/(2q) both prime (checked
+# by a sieve run when this restatement was written: k = 2,487,002 classes above the base).
+MODE4096, MODE4096_V2 = "Mode4096", "Mode4096_V2"
+_DELTAS = {
+    MODE4096: 495448529856135475846147600290107731951815687842437876083937612367400355133042233301,
+    MODE4096_V2: int("25f2da6646e943db028bd17d654a5fe9dc13e777f86b494195b2a55ba0d6d33e6d9d4f", 16),
+}
+EG1_G_PREFIX = "037DE384F98F6E038D2A3141825B33D5"  # published EG 1.0 generator, leading digits
 
 
-def derive_production_group() -> Tuple[int, int, int, int]:
-    """Re-derive (p, q, g, r) of the EG 1.0 4096-bit group from ln 2.
-
-    p = 2^4096 - 2^3840 + 2^256 * (floor(2^3584 ln2) + DELTA) + 2^256 - 1,
-    r = (p-1)/q, g = 2^r mod p.
-    """
+def derive_group(mode: str = MODE4096) -> Tuple[int, int, int, int]:
+    """Re-derive (p, q, g, r) of a 4096-bit group from its constant (gamma or ln 2)."""
     import mpmath
 
     with mpmath.workprec(3700):
-        x = int(mpmath.floor(mpmath.log(2) * mpmath.mpf(2) ** 3584))
-    p = 2**4096 - 2**3840 + 2**256 * (x + DELTA) + 2**256 - 1
+        c = mpmath.euler if mode == MODE4096 else mpmath.log(2)
+        x = int(mpmath.floor(c * mpmath.mpf(2) ** 3584))
+    d = _DELTAS[mode]
+    if mode == MODE4096:
+        p = 2**4096 - 2**3840 + 2**256 * (x + d) - 1
+    else:
+        p = 2**4096 - 2**3840 + 2**256 * (x + d) + 2**256 - 1
     assert (p - 1) % Q == 0, "q does not divide p-1: constants mis-derived"
     r = (p - 1) // Q
     g = pow(2, r, p)
     assert g != 1 and pow(g, Q, p) == 1
+    if mode == MODE4096:
+        assert f"{g:01024X}".startswith(EG1_G_PREFIX), "EG 1.0 generator prefix mismatch"
     return p, Q, g, r
 
 
-_GROUP_CACHE: Optional[Tuple[int, int, int, int]] = None
+def derive_production_group() -> Tuple[int, int, int, int]:
+    """KUtils.productionGroup() (KUtils.java:10-12): Mode4096, the EG 1.0 group."""
+    return derive_group(MODE4096)
 
 
-def production_group() -> "Group":
-    global _GROUP_CACHE
-    if _GROUP_CACHE is None:
-        _GROUP_CACHE = derive_production_group()
-    p, q, g, r = _GROUP_CACHE
+_GROUP_CACHE: Dict[str, Tuple[int, int, int, int]] = {}
+
+
+def production_group(mode: str = MODE4096) -> "Group":
+    if mode not in _GROUP_CACHE:
+        _GROUP_CACHE[mode] = derive_group(mode)
+    p, q, g, r = _GROUP_CACHE[mode]
     return Group(p, q, g)
 
 
@@ -205,9 +229,16 @@ def make_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, m: int, R: int
     return RangeProof(c_fake, v_fake, c_real, v_real)
 
 
+def is_valid_residue(G: Group, x: int) -> bool:
+    """ElementModP.isValidResidue (EG 1.0 verifier): 0 <= x < p and x^q == 1 mod p, i.e. x is
+    in the order-q subgroup.  The reference imports elements unchecked
+    (ConvertCommonProto.java:50-57) and leaves this to Verifier (RunRemoteWorkflowTest.java:179-182)."""
+    return 0 < x < G.p and pow(x, G.q, G.p) == 1
+
+
 def verify_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, pr: RangeProof) -> bool:
     q, p = G.q, G.p
-    if not (0 <= ct.pad < p and 0 <= ct.data < p):
+    if not (is_valid_residue(G, ct.pad) and is_valid_residue(G, ct.data)):
         return False
     if not all(0 <= x < q for x in (pr.c0, pr.v0, pr.c1, pr.v1)):
         return False
@@ -234,6 +265,10 @@ def make_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, R_sum: int,
 
 
 def verify_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, limit: int, pr: GenericProof) -> bool:
+    """Contest selection-limit proof over the aggregate message (A, B) = (prod alpha, prod beta);
+    like the range proof it requires the message to be valid residues."""
+    if not (is_valid_residue(G, A) and is_valid_residue(G, B)):
+        return False
     if not (0 <= pr.c < G.q and 0 <= pr.v < G.q):
         return False
     a, b = constant_commitments(G, K, A, B, limit, pr)

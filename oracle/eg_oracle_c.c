@@ -13,7 +13,8 @@
  *                    32 windows x 256 entries, product of 32 table entries
  *   hash           : SHA-256 over "|" + "|".join(upper-case fixed-width hex) + "|", mod q
  *                    (matches eg_oracle.py:hash_elems)
- * Verification follows eg_oracle.py:verify_range_proof / verify_constant_proof and the
+ * Verification (including the valid-residue tests x^q == 1 of every alpha, beta and of each
+ * contest's (A, B)) follows eg_oracle.py:verify_range_proof / verify_constant_proof and the
  * tally eg_oracle.py:accumulate_tally (Verifier / runAccumulateBallots at
  * RunRemoteWorkflowTest.java:151,179-182).  Multi-threaded over ballots (pthreads), as
  * the reference's Verifier(record, 11) is over 11 JVM threads.
@@ -41,7 +42,24 @@ static BIGNUM* Kbn = NULL;
 
 static BIGNUM* bn_be(const uint8_t* b, int n) { return BN_bin2bn(b, n, NULL); }
 
+static void radix_free(Radix** R) {
+  if (!*R) return;
+  for (int k = 0; k < 32; ++k)
+    for (int d = 0; d < 256; ++d) BN_free((*R)->t[k][d]);
+  free(*R);
+  *R = NULL;
+}
+
+/* (Re)initialise the group; tables of a previous group are dropped. */
 int ego_init(const uint8_t p[512], const uint8_t q[32], const uint8_t g[512]) {
+  radix_free(&RG);
+  radix_free(&RK);
+  if (G.p) {
+    BN_free(G.p);
+    BN_free(G.q);
+    BN_free(G.g);
+    BN_MONT_CTX_free(G.mont);
+  }
   BN_CTX* ctx = BN_CTX_new();
   G.p = bn_be(p, 512);
   G.q = bn_be(q, 32);
@@ -83,6 +101,7 @@ int ego_set_key(const uint8_t K[512]) {
   if (!RG) RG = radix_build(G.g);
   if (Kbn) BN_free(Kbn);
   Kbn = bn_be(K, 512);
+  radix_free(&RK);
   RK = radix_build(Kbn);
   return 0;
 }
@@ -148,6 +167,11 @@ static void* verify_worker(void* arg) {
         BN_bin2bn(pr + 96, 32, v1);
         int ok = BN_cmp(al, G.p) < 0 && BN_cmp(be, G.p) < 0 && BN_cmp(c0, G.q) < 0 && BN_cmp(v0, G.q) < 0 &&
                  BN_cmp(c1, G.q) < 0 && BN_cmp(v1, G.q) < 0;
+        /* valid residues: alpha^q == 1 and beta^q == 1 (eg_oracle.py:is_valid_residue) */
+        BN_mod_exp_mont(t1, al, G.q, G.p, ctx, G.mont);
+        ok = ok && BN_is_one(t1);
+        BN_mod_exp_mont(t1, be, G.q, G.p, ctx, G.mont);
+        ok = ok && BN_is_one(t1);
         /* a0 = g^v0 al^c0 ; b0 = K^v0 be^c0 ; a1 = g^v1 al^c1 ; b1 = K^v1 be^c1 g^-c1 */
         radix_pow(t1, RG, pr + 32, ctx);
         BN_mod_exp_mont(t2, al, c0, G.p, ctx, G.mont);
@@ -179,6 +203,10 @@ static void* verify_worker(void* arg) {
       BN_bin2bn(cp, 32, c0);
       BN_bin2bn(cp + 32, 32, v0);
       int ok = BN_cmp(c0, G.q) < 0 && BN_cmp(v0, G.q) < 0;
+      BN_mod_exp_mont(t1, A, G.q, G.p, ctx, G.mont); /* (A, B) valid residues */
+      ok = ok && BN_is_one(t1);
+      BN_mod_exp_mont(t1, B, G.q, G.p, ctx, G.mont);
+      ok = ok && BN_is_one(t1);
       radix_pow(t1, RG, cp + 32, ctx);
       BN_mod_exp_mont(t2, A, c0, G.p, ctx, G.mont);
       mulp(a0, t1, t2, ctx);

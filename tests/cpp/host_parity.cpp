@@ -1,7 +1,7 @@
 // host_parity.cpp -- parity driver for the C++ host mirror (electionguard-remote_amd/host/
 // electionguard.hpp) over the C ABI.  Run by tests/test_cpp_host.py:
 //   host_parity cpu               host-only checks (mod-q arithmetic, constants, ABI info)
-//   host_parity gpu <vectors>     golden vectors (tests/golden/*.json flattened to text by
+//   host_parity gpu <vectors> [V2] golden vectors (tests/golden/<mode>/*.json flattened to text by
 //                                 the test) through the C++ API, then a 5-guardian /
 //                                 quorum-3 decryption with 2 missing guardians (config 4
 //                                 shape) that must recover the exact counts.
@@ -92,8 +92,8 @@ static std::vector<std::string> split(const std::string& line) {
   return t;
 }
 
-static int run_gpu(const char* path) {
-  GroupContext& G = GroupContext::productionGroup(0);
+static int run_gpu(const char* path, ProductionMode mode) {
+  GroupContext& G = GroupContext::productionGroup(0, mode);
   std::ifstream in(path);
   if (!in) {
     std::cerr << "cannot open " << path << std::endl;
@@ -262,11 +262,13 @@ static int run_gpu(const char* path) {
 int main(int argc, char** argv) {
   try {
     if (argc >= 2 && std::string(argv[1]) == "cpu") return run_cpu();
-    if (argc >= 3 && std::string(argv[1]) == "gpu") return run_gpu(argv[2]);
+    if (argc >= 3 && std::string(argv[1]) == "gpu")
+      return run_gpu(argv[2], argc >= 4 && std::string(argv[3]) == "V2" ? ProductionMode::Mode4096_V2
+                                                                          : ProductionMode::Mode4096);
   } catch (const std::exception& e) {
     std::cerr << "exception: " << e.what() << std::endl;
     return 1;
   }
-  std::cerr << "usage: host_parity cpu | gpu <vectors.txt>" << std::endl;
+  std::cerr << "usage: host_parity cpu | gpu <vectors.txt> [V2]" << std::endl;
   return 2;
 }

@@ -4,6 +4,8 @@ The reference (JohnLCaron/electionguard-remote) holds no fixtures or known-answe
 for this path and its arithmetic dependency cannot run here, so these
 vectors are produced by the oracle restatement and cross-checked against the
 independent OpenSSL-BN restatement (oracle/eg_oracle_c.c) by tests/test_oracle_golden.py.
+Both production groups get a full set (tests/golden/<ProductionMode>/*.json):
+Mode4096 (EG 1.0, the reference's group) and Mode4096_V2 (EG 2.0, named option).
 Run:  python tests/golden/make_golden.py   (deterministic; seeds below)
 """
 import json
@@ -95,11 +97,14 @@ def trustee(G):
 
 
 if __name__ == "__main__":
-    G = O.production_group()
-    (HERE / "group_ops.json").write_text(json.dumps(group_ops(G), indent=0))
-    (HERE / "ballots.json").write_text(json.dumps(ballots(G), indent=0))
-    (HERE / "trustee.json").write_text(json.dumps(trustee(G), indent=0))
-    p, q, g, r = O.derive_production_group()
-    (HERE / "constants.json").write_text(json.dumps({"p": hx(p, 512), "q": hx(q, 32), "g": hx(g, 512),
-                                                     "r": hx(r, 512)}, indent=0))
+    for mode in (O.MODE4096, O.MODE4096_V2):
+        out = HERE / mode
+        out.mkdir(exist_ok=True)
+        G = O.production_group(mode)
+        (out / "group_ops.json").write_text(json.dumps(group_ops(G), indent=0))
+        (out / "ballots.json").write_text(json.dumps(ballots(G), indent=0))
+        (out / "trustee.json").write_text(json.dumps(trustee(G), indent=0))
+        p, q, g, r = O.derive_group(mode)
+        (out / "constants.json").write_text(json.dumps({"mode": mode, "p": hx(p, 512), "q": hx(q, 32),
+                                                        "g": hx(g, 512), "r": hx(r, 512)}, indent=0))
     print("written")

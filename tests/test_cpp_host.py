@@ -2,7 +2,7 @@
 
 CPU: the mirror builds, its mod-q scalar arithmetic and constants self-check, and the
 generated constants header matches electionguard/core/constants.py.
-GPU: the golden vectors (tests/golden/*.json) through the C++ GroupContext /
+GPU: the golden vectors of both groups (tests/golden/<mode>/*.json) through the C++ GroupContext /
 GpuDecryptingTrustee API, bit-exact, then a 5-guardian quorum-3 decryption with two
 missing guardians recovering exact counts (tests/cpp/host_parity.cpp).
 """
@@ -37,9 +37,9 @@ def test_cpp_host_cpu_selfcheck():
     assert r.stdout.startswith("OK")
 
 
-def write_vectors(path: Path) -> int:
-    g = json.loads((GOLD / "group_ops.json").read_text())
-    t = json.loads((GOLD / "trustee.json").read_text())
+def write_vectors(path: Path, mode: str = "Mode4096") -> int:
+    g = json.loads((GOLD / mode / "group_ops.json").read_text())
+    t = json.loads((GOLD / mode / "trustee.json").read_text())
     lines = []
     lines += [f"powP {v['b']} {v['e']} {v['r']}" for v in g["powP"]]
     lines += [f"gPowP {v['e']} {v['r']}" for v in g["gPowP"]]
@@ -63,9 +63,11 @@ def test_vector_file_covers_golden(tmp_path):
 
 
 @pytest.mark.gpu
-def test_cpp_host_gpu_parity(tmp_path):
+@pytest.mark.parametrize("mode", ["Mode4096", "Mode4096_V2"])
+def test_cpp_host_gpu_parity(tmp_path, mode):
     v = tmp_path / "vectors.txt"
-    write_vectors(v)
-    r = subprocess.run([str(_bin()), "gpu", str(v)], capture_output=True, text=True, timeout=300)
+    write_vectors(v, mode)
+    args = [str(_bin()), "gpu", str(v)] + (["V2"] if mode == "Mode4096_V2" else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK")

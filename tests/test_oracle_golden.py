@@ -1,6 +1,8 @@
 """CPU: pin the oracle.  The reference has no fixtures for this path, so
 the golden vectors come from oracle/eg_oracle.py and are cross-checked here against the
-independent OpenSSL-BN restatement (oracle/eg_oracle_c.c) and the constants' self-checks."""
+independent OpenSSL-BN restatement (oracle/eg_oracle_c.c) and the constants' self-checks.
+Every fixture exists for both production groups (tests/golden/<ProductionMode>/):
+Mode4096 (EG 1.0, the reference's group) and Mode4096_V2 (EG 2.0)."""
 import json
 import random
 from pathlib import Path
@@ -11,33 +13,48 @@ import pytest
 import eg_oracle as O
 
 GOLD = Path(__file__).resolve().parent / "golden"
+MODES = (O.MODE4096, O.MODE4096_V2)
 
 
-def load(name):
-    return json.loads((GOLD / name).read_text())
+def load(name, mode=O.MODE4096):
+    return json.loads((GOLD / mode / name).read_text())
 
 
 def h(s):
     return int(s, 16)
 
 
-def test_constants_derivation_and_selfchecks():
+@pytest.mark.parametrize("mode", MODES)
+def test_constants_derivation_and_selfchecks(mode):
     import sympy
     from electionguard.core import constants as C
-    p, q, g, r = O.derive_production_group()
-    gold = load("constants.json")
+    p, q, g, r = O.derive_group(mode)
+    gold = load("constants.json", mode)
     assert (p, q, g, r) == (h(gold["p"]), h(gold["q"]), h(gold["g"]), h(gold["r"]))
-    assert (p, q, g, r) == (C.P, C.Q, C.G, C.R)          # product constants == oracle derivation
+    c = C.constants_for(mode)
+    assert (p, q, g, r) == (c.p, c.q, c.g, c.r)          # product constants == oracle derivation
     assert q == 2**256 - 189 and p.bit_length() == 4096
     assert (p - 1) % q == 0 and r * q + 1 == p
     assert pow(g, q, p) == 1 and g != 1 and g == pow(2, r, p)
-    assert sympy.isprime(q) and sympy.isprime(p)
+    assert sympy.isprime(q) and sympy.isprime(p) and sympy.isprime(r // 2)
     assert p % 2**256 == 2**256 - 1                       # Montgomery-friendly: -p^-1 = 1 mod 2^256
 
 
-def test_python_oracle_reproduces_group_golden(oracle_group):
-    G = oracle_group
-    d = load("group_ops.json")
+def test_reference_group_is_the_eg1_gamma_group():
+    """Mode4096 (the default everywhere) is built from Euler's gamma and reproduces the
+    published EG 1.0 generator; the ln 2 group is only the named V2 option."""
+    from electionguard.core import constants as C
+    assert C.P == C.MODE4096.p and C.G == C.MODE4096.g
+    assert f"{C.P:01024X}"[64:96] == "93C467E37DB0C7A4D1BE3F810152CB56"   # gamma = 0.93C467E3...h
+    assert f"{C.G:01024X}".startswith(O.EG1_G_PREFIX)
+    assert f"{C.MODE4096_V2.p:01024X}"[64:80] == "B17217F7D1CF79AB"        # ln 2 = 0.B17217F7...h
+    assert O.production_group().p == C.P
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_python_oracle_reproduces_group_golden(mode):
+    G = O.production_group(mode)
+    d = load("group_ops.json", mode)
     for v in d["powP"]:
         assert G.powP(h(v["b"]), h(v["e"])) == h(v["r"])
     for v in d["gPowP"][:8]:
@@ -55,19 +72,20 @@ def _arr(hexes, n):
     return np.stack([np.frombuffer(bytes.fromhex(x), np.uint8) for x in hexes]).reshape(-1, n)
 
 
-def test_c_oracle_agrees_on_group_golden(oracle_group):
+@pytest.mark.parametrize("mode", MODES)
+def test_c_oracle_agrees_on_group_golden(mode):
     from eg_oracle_c import COracle
-    G = oracle_group
+    G = O.production_group(mode)
     co = COracle(G.p, G.q, G.g)
-    d = load("group_ops.json")
+    d = load("group_ops.json", mode)
     out = co.powp(_arr([v["b"] for v in d["powP"]], 512), _arr([v["e"] for v in d["powP"]], 32))
     assert [x.tobytes().hex() for x in out] == [v["r"] for v in d["powP"]]
     out = co.gpowp(_arr([v["e"] for v in d["gPowP"]], 32))
     assert [x.tobytes().hex() for x in out] == [v["r"] for v in d["gPowP"]]
 
 
-def golden_ballot_arrays():
-    d = load("ballots.json")
+def golden_ballot_arrays(mode=O.MODE4096):
+    d = load("ballots.json", mode)
     nc, ns, va = d["manifest"]
     spc = ns + va
     nb = len(d["ballots"])
@@ -82,10 +100,11 @@ def golden_ballot_arrays():
     return d, (nc, ns, va, spc), cts, rp, cp
 
 
-def test_c_oracle_verifies_golden_ballots_and_tally(oracle_group):
+@pytest.mark.parametrize("mode", MODES)
+def test_c_oracle_verifies_golden_ballots_and_tally(mode):
     from eg_oracle_c import COracle
-    G = oracle_group
-    d, (nc, ns, va, spc), cts, rp, cp = golden_ballot_arrays()
+    G = O.production_group(mode)
+    d, (nc, ns, va, spc), cts, rp, cp = golden_ballot_arrays(mode)
     co = COracle(G.p, G.q, G.g)
     co.set_key(h(d["K"]))
     ok_s, ok_c, tally = co.verify_ballots(h(d["qbar"]), nc, spc, va, va, cts, rp, cp, threads=2)
@@ -97,17 +116,18 @@ def test_c_oracle_verifies_golden_ballots_and_tally(oracle_group):
     assert not ok_s[1, 2] and ok_s.sum() == ok_s.size - 1
 
 
-def test_python_oracle_trustee_golden(oracle_group):
-    G = oracle_group
-    d = load("trustee.json")
+@pytest.mark.parametrize("mode", MODES)
+def test_python_oracle_trustee_golden(mode):
+    G = O.production_group(mode)
+    d = load("trustee.json", mode)
     qbar = h(d["qbar"])
     gs = [O.Guardian(f"guardian{g['x']}", g["x"], [h(a) for a in g["coeffs"]], [h(k) for k in g["commitments"]])
           for g in d["guardians"]]
     texts = [O.Ciphertext(h(a), h(b)) for a, b in d["texts"]]
     nonces = [h(u) for u in d["nonces"]]
-    for (M, pr), want in zip(O.direct_decrypt(G, qbar, gs[0], texts, nonces), d["direct"]):
+    for i, ((M, pr), want) in enumerate(zip(O.direct_decrypt(G, qbar, gs[0], texts, nonces), d["direct"])):
         assert (M, pr.c, pr.v) == (h(want["M"]), h(want["c"]), h(want["v"]))
-        assert O.verify_share(G, qbar, gs[0].K, texts[0] if False else texts[d["direct"].index(want)], M, pr)
+        assert O.verify_share(G, qbar, gs[0].K, texts[i], M, pr)
 
 
 def test_hash_host_matches_oracle():
@@ -116,3 +136,93 @@ def test_hash_host_matches_oracle():
     for _ in range(5):
         els = [("Q", rng.randrange(2**256))] + [("P", rng.randrange(2**4096)) for _ in range(3)]
         assert hash_elems(O.Q, *els) == O.hash_elems(O.Q, *els)
+
+
+# --------------------------------------------------------------------------------------
+# Residue (subgroup) validation: a ballot whose alpha is multiplied by p-1 (order 2) while
+# its proofs are re-made to match.  Without the x^q == 1 tests every proof verifies.
+# --------------------------------------------------------------------------------------
+
+def forge_negated_alpha(G, K, qbar, man, votes, rng, sel):
+    """Encrypt a ballot, then replace selection `sel`'s alpha by (p-1)*alpha = -alpha and
+    re-make its range proof and its contest's constant proof so that every Fiat-Shamir
+    check passes on the forged ciphertext: the real-branch recompute g^v (-alpha)^c equals
+    g^u exactly when c is even, so the prover retries its nonces until both challenges are
+    even.  Returns (ballot, the honest nonces R per selection)."""
+    q = G.q
+    spc = man.sel_per_contest
+    Rs = [rng.randrange(1, q) for _ in votes]
+    cts = [O.encrypt(G, K, m, R) for m, R in zip(votes, Rs)]
+    cts[sel] = O.Ciphertext((G.p - 1) * cts[sel].pad % G.p, cts[sel].data)
+    proofs, cproofs = [], []
+    for i, (ct, m, R) in enumerate(zip(cts, votes, Rs)):
+        while True:
+            pr = O.make_range_proof(G, K, qbar, ct, m, R, rng.randrange(1, q), rng.randrange(q), rng.randrange(q))
+            c_real = pr.c0 if m == 0 else pr.c1
+            if i != sel or c_real % 2 == 0:
+                break
+        proofs.append(pr)
+    for c in range(man.n_contests):
+        sl = slice(c * spc, (c + 1) * spc)
+        A = G.prodP([ct.pad for ct in cts[sl]])
+        B = G.prodP([ct.data for ct in cts[sl]])
+        R_sum = sum(Rs[sl]) % q
+        while True:
+            cpr = O.make_constant_proof(G, K, qbar, A, B, R_sum, rng.randrange(1, q))
+            if not (c * spc <= sel < (c + 1) * spc) or cpr.c % 2 == 0:
+                break
+        cproofs.append(cpr)
+    return O.EncryptedBallot(cts, proofs, cproofs)
+
+
+def _proof_checks_without_residues(G, K, qbar, man, eb):
+    """The verifier's Fiat-Shamir equations alone (no residue tests)."""
+    spc = man.sel_per_contest
+    ok = []
+    for i, (ct, pr) in enumerate(zip(eb.cts, eb.proofs)):
+        a0, b0, a1, b1 = O.range_commitments(G, K, ct, pr)
+        ok.append((pr.c0 + pr.c1) % G.q == O.range_challenge(G, qbar, ct, a0, b0, a1, b1))
+    for c in range(man.n_contests):
+        A = G.prodP([ct.pad for ct in eb.cts[c * spc:(c + 1) * spc]])
+        B = G.prodP([ct.data for ct in eb.cts[c * spc:(c + 1) * spc]])
+        a, b = O.constant_commitments(G, K, A, B, man.votes_allowed, eb.contest_proofs[c])
+        ok.append(eb.contest_proofs[c].c == O.constant_challenge(G, qbar, A, B, a, b))
+    return ok
+
+
+def residue_forgery_case(seed=77):
+    G = O.production_group()
+    rng = random.Random(seed)
+    gs, K = O.key_ceremony(G, 2, 2, rng)
+    qbar = rng.randrange(G.q)
+    man = O.Manifest(2, 2, 1)
+    votes = O.ballot_plaintexts(man, rng)
+    sel = 1
+    eb = forge_negated_alpha(G, K, qbar, man, votes, rng, sel)
+    return G, K, qbar, man, eb, sel
+
+
+def test_oracle_rejects_non_residue_alpha_with_matching_proofs():
+    G, K, qbar, man, eb, sel = residue_forgery_case()
+    assert all(_proof_checks_without_residues(G, K, qbar, man, eb))   # the forgery is complete
+    assert not O.is_valid_residue(G, eb.cts[sel].pad)
+    ok_sel = [O.verify_range_proof(G, K, qbar, ct, pr) for ct, pr in zip(eb.cts, eb.proofs)]
+    assert ok_sel == [i != sel for i in range(len(eb.cts))]
+    assert not O.verify_ballot(G, K, qbar, man, eb)
+    spc = man.sel_per_contest
+    A = G.prodP([ct.pad for ct in eb.cts[:spc]])
+    assert not O.is_valid_residue(G, A)                                  # the contest is flagged too
+
+
+def test_c_oracle_rejects_non_residue_alpha():
+    from eg_oracle_c import COracle
+    G, K, qbar, man, eb, sel = residue_forgery_case()
+    b = lambda x, n: np.frombuffer(int(x).to_bytes(n, "big"), np.uint8)
+    cts = np.stack([np.stack([b(ct.pad, 512), b(ct.data, 512)]) for ct in eb.cts])[None]
+    rp = np.stack([np.stack([b(v, 32) for v in (pr.c0, pr.v0, pr.c1, pr.v1)]) for pr in eb.proofs])[None]
+    cp = np.stack([np.stack([b(pr.c, 32), b(pr.v, 32)]) for pr in eb.contest_proofs])[None]
+    co = COracle(G.p, G.q, G.g)
+    co.set_key(K)
+    ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, man.sel_per_contest, 1, 1, cts, rp, cp, tally=False)
+    assert ok_s[0].tolist() == [i != sel for i in range(len(eb.cts))]
+    assert ok_c[0].tolist() == [False, True]
