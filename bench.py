@@ -39,8 +39,9 @@ def parse():
     ap.add_argument("--contests", type=int, default=4)
     ap.add_argument("--selections", type=int, default=5)
     ap.add_argument("--fb-window", type=int, default=22, help="fixed-base radix window bits for g and K")
-    ap.add_argument("--cpu-sample", type=int, default=256, help="ballots for the CPU baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=1, help="run the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the affinity count)")
     ap.add_argument("--modexp-n", type=int, default=1 << 20,
                     help="modexp microbenchmark batch per GPU (SURVEY 8(d): 2^20; 0 = skip)")
     return ap.parse_args()
@@ -48,7 +49,15 @@ def parse():
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    from electionguard.launch import launched_world, run_ranks
+    lw = launched_world()
+    if lw is None and a.gpus > 1:
+        # no launcher: start one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*) before
+        # anything touches HIP; rank 0 prints the JSON line, this parent returns the worst status
+        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus))
+    if lw is not None and lw != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={lw} ranks")
+    world = lw or 1
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -142,10 +151,7 @@ def main():
     import hashlib
     build_id = hashlib.md5(Path(native.lib_path()).read_bytes()).hexdigest()[:12]
     total_ballots = nb * world * a.steps
-    # configs[1] = the 4x5 bench default; configs[4] = the 100-selection manifest (20 x 5)
-    cfg_name = {(4, 5): "configs[1]", (20, 5): "configs[4] shape"}.get((a.contests, a.selections), "custom manifest")
-    if (a.contests, a.selections) == (4, 5) and nb * world == 1_000_000:
-        cfg_name = f"configs[2] (1M ballots over {world} GPU{'s' if world > 1 else ''})"
+    cfg_name = config_name(a.contests, a.selections, nb, world)
     coll = "RCCL" if (dist is None or backend == "nccl") else backend
     value = total_ballots / el
     # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
@@ -219,6 +225,22 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def config_name(contests: int, selections: int, nb: int, world: int) -> str:
+    """BASELINE.json config this run measures: configs[1] = 10k ballots of 4 x 5 on ONE GPU;
+    configs[2] = 1M ballots of 4 x 5 over the node; configs[4] = the 100-selection manifest."""
+    total = nb * world
+    gpus = f"{world} GPU{'s' if world > 1 else ''}"
+    if (contests, selections) == (4, 5):
+        if total == 1_000_000:
+            return f"configs[2] (1M ballots over {gpus})"
+        if world == 1 and nb == 10_000:
+            return "configs[1]"
+        return f"configs[1] shape (4x5), {nb} ballots per GPU x {gpus}"
+    if (contests, selections) == (20, 5):
+        return f"configs[4] shape (20x5), {nb} ballots per GPU x {gpus}"
+    return f"custom manifest {contests}x{selections}, {nb} ballots per GPU x {gpus}"
 
 
 def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2):
@@ -302,20 +324,47 @@ def modexp_ubench(group, n, dev, rank, reps=2):
 
 def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
     """C restatement of the JVM path (OpenSSL BN Montgomery sliding window, 8-bit radix
-    fixed base = LOW_MEMORY_USE) on a bounded sample of the same ballots."""
+    fixed base = LOW_MEMORY_USE) on a bounded sample of the same ballots, on every host core
+    this process may run on (sched_getaffinity), sized to about --cpu-seconds of work."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from eg_oracle_c import COracle
     from electionguard.core import constants as C
 
-    threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    affinity = len(os.sched_getaffinity(0))
+    quota_cpus = None
+    try:  # a cgroup CPU quota caps the useful parallelism below the affinity count
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q and q[0] != "max":
+            quota_cpus = int(q[0]) / int(q[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    # every core the lease lets this process use: the affinity set, capped by the CPU quota
+    # (more threads than the quota only time-slice: 256 threads under a 16-CPU quota ran 38% slower)
+    threads = a.cpu_threads or max(1, min(affinity, int(quota_cpus + 0.5) if quota_cpus else affinity))
     co = COracle(C.P, C.Q, C.G)
     co.set_key(K)
-    s = min(a.cpu_sample, eb.n)
-    sub = eb.slice(0, s)
+
+    def run(n):
+        sub = eb.slice(0, n)
+        t = time.perf_counter()
+        ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, man.spc, 1, 1, sub.cts, sub.rproof, sub.cproof,
+                                          threads=threads)
+        return time.perf_counter() - t, bool(ok_s.all() and ok_c.all())
+
+    n0 = min(eb.n, 2 * threads)
+    dt0, _ = run(n0)  # calibration (also warms the radix tables' caches)
+    s = max(n0, min(eb.n, int(n0 / dt0 * a.cpu_seconds)))
+    dt, valid = run(s)
+    # per-core variable-base modexp rate (256-bit exponents, BN_mod_exp_mont, one thread)
+    rng = np.random.default_rng(11)
+    nb_pow = 256
+    bases = np.stack([np.frombuffer(pow(C.G, int(x), C.P).to_bytes(512, "big"), np.uint8)
+                      for x in rng.integers(1, 2**62, size=nb_pow)])
+    exps = rng.integers(0, 256, size=(nb_pow, 32), dtype=np.uint8)
     t = time.perf_counter()
-    ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, man.spc, 1, 1, sub.cts, sub.rproof, sub.cproof,
-                                      threads=threads)
-    dt = time.perf_counter() - t
+    co.powp(bases, exps)
+    per_core_modexp = nb_pow / (time.perf_counter() - t)
+    quota = f", cgroup CPU quota {quota_cpus:.1f}" if quota_cpus else ", no cgroup CPU quota"
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -329,9 +378,14 @@ def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
         "unit": "ballots/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{s} of the same ballots (verify+tally, {man.nsel} selections each), {threads} threads "
-                  f"on {model or 'host CPU'}; OpenSSL BN_mod_exp_mont + 8-bit radix fixed base; "
-                  f"verdicts all valid: {bool(ok_s.all() and ok_c.all())}; wall {dt:.2f} s",
+        "sample": f"{s} of the same ballots (verify incl. residue tests + tally, {man.nsel} selections each), "
+                  f"{threads} threads = the lease's usable CPUs (affinity {affinity} of {os.cpu_count()}{quota}) on "
+                  f"{model or 'host CPU'}; OpenSSL BN_mod_exp_mont + 8-bit radix fixed base; "
+                  f"verdicts all valid: {valid}; wall {dt:.2f} s",
+        "cpu_model": model,
+        "affinity_cpus": affinity,
+        "cgroup_quota_cpus": quota_cpus,
+        "var_base_modexp_per_s_per_core": round(per_core_modexp, 1),
     }
 
 

@@ -169,6 +169,7 @@ class Verifier:
                       d_tally: Optional[int]) -> None:
         """Asynchronous verify on device pointers (e.g. torch CUDA tensors' data_ptr())."""
         man, g = self.man, self.group
+        self.key.ensure()  # the ctx may hold another key since this Verifier was made (no-op if not)
         native.check(g._lib, "eg_verify_ballots_dev",
                      g._lib.eg_verify_ballots_dev(g.handle, native.buf(self._qb), nb, man.n_contests, man.spc,
                                                   man.votes_allowed, man.votes_allowed, d_cts, d_rproof, d_cproof,

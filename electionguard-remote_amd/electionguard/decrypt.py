@@ -283,7 +283,8 @@ class Decryption:
 
 
 def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionRecord, public_keys: Dict[str, int],
-                             commitments: Dict[str, List[int]]) -> Dict[str, bool]:
+                             commitments: Dict[str, List[int]], guardian_xs: Optional[Dict[str, int]] = None,
+                             quorum: Optional[int] = None, max_count: Optional[int] = None) -> Dict[str, bool]:
     """Record-level checks of the tally decryption (the decryption part of the reference's
     ``Verifier(record, 11).verify()``, RunRemoteWorkflowTest.java:179-182; EG 1.0 spec
     verification steps for partial / compensated decryptions and the plaintext tally),
@@ -297,13 +298,22 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
                                the same set of available guardians, each with a direct share;
       * ``tally``              B == M * g^t per text with M = prod_i M_i * prod_l prod_i
                                M_{l,i}^{w_i} (Lagrange w_i over the available x's) and t
-                               the published count.
+                               the published count (an integer in [0, max_count]).
+    With the key ceremony's view (``guardian_xs``: every guardian's x-coordinate, ``quorum``)
+    the quorum check also requires the record's x's to be the ceremony's, at least ``quorum``
+    available guardians, and available + missing = all guardians.
     """
     G = group
     T = rec.texts
     n = len(T)
     out = {"direct_proofs": True, "recovery_keys": True, "compensated_proofs": True, "quorum": True, "tally": True}
     avail = list(rec.direct)
+    if guardian_xs is not None:
+        out["quorum"] &= all(rec.xs.get(g) == x for g, x in guardian_xs.items() if g in rec.xs)
+        out["quorum"] &= all(g in guardian_xs for g in rec.xs)
+        out["quorum"] &= sorted(avail + list(rec.compensated)) == sorted(guardian_xs)
+    if quorum is not None:
+        out["quorum"] &= len(avail) >= quorum
     for gid in avail:
         res = rec.direct[gid]
         if gid not in public_keys or gid not in rec.xs:
@@ -312,7 +322,9 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
         out["direct_proofs"] &= len(res) == n and bool(
             verify_shares(G, qbar, [public_keys[gid]] * n, T, [r.partialDecryption for r in res],
                           [r.proof for r in res]).all())
-    if len(rec.counts) != n or any(c is None for c in rec.counts):
+    if len(rec.counts) != n or any(
+            c is None or not isinstance(c, (int, np.integer)) or c < 0 or (max_count is not None and c > max_count)
+            for c in rec.counts):
         out["tally"] = False
     for l, by_avail in rec.compensated.items():
         out["quorum"] &= sorted(by_avail) == sorted(avail)

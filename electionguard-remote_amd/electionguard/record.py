@@ -53,10 +53,16 @@ def verify_election_record(group: GroupContext, rec: ElectionRecord, window_bits
     out: Dict[str, bool] = {}
     comm = [k for g in rec.guardians for k in g.commitments]
     prf = [p for g in rec.guardians for p in g.proofs]
-    out["guardian_proofs"] = len(comm) == len(prf) and all(verify_commitment_proofs(group, comm, prf))
-    k0 = as_p_array([g.commitments[0] for g in rec.guardians])
-    K = int.from_bytes(group.prodP_groups(k0, 1, len(rec.guardians))[0].tobytes(), "big")
-    out["joint_key"] = K == rec.joint_key
+    # every guardian commits to a polynomial of the same degree: quorum = its coefficient count
+    shapes_ok = bool(rec.guardians) and all(g.commitments for g in rec.guardians) and \
+        len({len(g.commitments) for g in rec.guardians}) == 1
+    out["guardian_proofs"] = shapes_ok and len(comm) == len(prf) and all(verify_commitment_proofs(group, comm, prf))
+    if shapes_ok:
+        k0 = as_p_array([g.commitments[0] for g in rec.guardians])
+        K = int.from_bytes(group.prodP_groups(k0, 1, len(rec.guardians))[0].tobytes(), "big")
+        out["joint_key"] = K == rec.joint_key
+    else:
+        out["joint_key"] = False
     man = rec.manifest
     key = ElectionKey(group, rec.joint_key, window_bits=window_bits)
     ok_s, ok_c, tally = Verifier(group, key, rec.qbar, man).verify(rec.ballots)
@@ -65,9 +71,12 @@ def verify_election_record(group: GroupContext, rec: ElectionRecord, window_bits
     out["tally"] = et.shape == tally.shape and bool(np.array_equal(et, tally))
     dtexts = np.ascontiguousarray(rec.decryption.texts, dtype=np.uint8).reshape(-1, 2, 512)
     same_texts = dtexts.shape == et.shape and bool(np.array_equal(dtexts, et))
-    pks = {g.gid: g.commitments[0] for g in rec.guardians}
-    commitments = {g.gid: g.commitments for g in rec.guardians}
-    dv = verify_decryption_record(group, rec.qbar, rec.decryption, pks, commitments)
+    pks = {g.gid: g.commitments[0] for g in rec.guardians if g.commitments}
+    commitments = {g.gid: g.commitments for g in rec.guardians if g.commitments}
+    dv = verify_decryption_record(group, rec.qbar, rec.decryption, pks, commitments,
+                                  guardian_xs={g.gid: g.x for g in rec.guardians},
+                                  quorum=len(rec.guardians[0].commitments) if shapes_ok else None,
+                                  max_count=rec.ballots.n)
     out["decryption.texts"] = same_texts
     for name, ok in dv.items():
         out[f"decryption.{name}"] = ok

@@ -740,28 +740,36 @@ inline DecryptionRecordChecks verifyDecryptionRecord(const GroupContext& G, cons
                                                      const DecryptionRecord& rec,
                                                      const std::map<std::string, ElementModP>& publicKeys,
                                                      const std::map<std::string, std::vector<ElementModP>>& commitments) {
+  // Malformed (untrusted) records fail their checks instead of throwing or reading out of
+  // bounds: unknown guardian ids, short share lists and negative counts are all "false".
   DecryptionRecordChecks out;
   const size_t n = rec.texts.size();
   auto allTrue = [](const std::vector<bool>& v) { return std::find(v.begin(), v.end(), false) == v.end(); };
   for (const auto& [gid, res] : rec.direct) {
+    const auto pk = publicKeys.find(gid);
+    if (pk == publicKeys.end() || rec.xs.count(gid) == 0) { out.directProofs = out.quorum = false; continue; }
     if (res.size() != n) { out.directProofs = false; continue; }
     std::vector<ElementModP> M;
     std::vector<GenericChaumPedersenProof> pr;
     for (const auto& r : res) { M.push_back(r.partialDecryption); pr.push_back(r.proof); }
-    out.directProofs &= allTrue(verifyShares(G, qbar, std::vector<ElementModP>(n, publicKeys.at(gid)), rec.texts, M, pr));
+    out.directProofs &= allTrue(verifyShares(G, qbar, std::vector<ElementModP>(n, pk->second), rec.texts, M, pr));
   }
   if (rec.counts.size() != n) out.tally = false;
-  for (const auto& c : rec.counts) out.tally &= c.has_value();
+  for (const auto& c : rec.counts) out.tally &= c.has_value() && *c >= 0;
   for (const auto& [l, byAvail] : rec.compensated) {
     out.quorum &= byAvail.size() == rec.direct.size();
+    const auto cm = commitments.find(l);
+    if (cm == commitments.end()) { out.recoveryKeys = out.compensatedProofs = false; continue; }
+    const auto& comm = cm->second;
     for (const auto& [gid, res] : byAvail) {
       out.quorum &= rec.direct.count(gid) == 1;
+      const auto xi = rec.xs.find(gid);
+      if (xi == rec.xs.end() || xi->second < 0) { out.quorum = false; continue; }
       if (res.size() != n) { out.compensatedProofs = out.recoveryKeys = false; continue; }
       // g^{P_l(x_i)} = prod_j K_{l,j}^{x_i^j}
-      const auto& comm = commitments.at(l);
       std::vector<ElementModQ> e;
       ElementModQ xj = G.uIntToElementModQ(1);
-      const ElementModQ x = G.uIntToElementModQ((uint64_t)rec.xs.at(gid));
+      const ElementModQ x = G.uIntToElementModQ((uint64_t)xi->second);
       for (size_t j = 0; j < comm.size(); ++j) { e.push_back(xj); xj = G.mulQ(xj, x); }
       const ElementModP want = G.multP(G.powPBatch(comm, e));
       std::vector<ElementModP> M, rk;
@@ -773,10 +781,16 @@ inline DecryptionRecordChecks verifyDecryptionRecord(const GroupContext& G, cons
       out.compensatedProofs &= allTrue(verifyShares(G, qbar, rk, rec.texts, M, pr));
     }
   }
+  // every share list must cover every text before the combination indexes them
+  bool lengthsOk = true;
+  for (const auto& [gid, res] : rec.direct) lengthsOk &= res.size() == n;
+  for (const auto& [l, byAvail] : rec.compensated)
+    for (const auto& [gid, res] : byAvail) lengthsOk &= res.size() == n;
+  if (!lengthsOk) out.tally = false;
   if (!out.quorum || !out.tally || n == 0) return out;
-  // B == M g^t with M = prod_i M_i * prod_l prod_i M_{l,i}^{w_i}
+  // B == M g^t with M = prod_i M_i * prod_l prod_i M_{l,i}^{w_i}; Lagrange over the AVAILABLE x's
   std::vector<int> xs;
-  for (const auto& [gid, x] : rec.xs) xs.push_back(x);
+  for (const auto& [gid, res] : rec.direct) xs.push_back(rec.xs.at(gid));
   std::vector<std::vector<ElementModP>> parts;
   for (const auto& [gid, res] : rec.direct) {
     std::vector<ElementModP> M;

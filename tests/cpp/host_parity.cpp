@@ -252,6 +252,27 @@ static int run_gpu(const char* path, ProductionMode mode) {
     rk = G.multPBatch({rk}, {G.gPowP(G.uIntToElementModQ(1))})[0];
     chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
     EXPECT(!chk.recoveryKeys && !chk.compensatedProofs && chk.tally && chk.directProofs, "tampered recovery key flagged");
+    // malformed records: flagged, never an exception or an out-of-bounds read
+    bad = rec;
+    bad.direct.begin()->second.pop_back();
+    chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.directProofs && !chk.tally, "short direct share list flagged");
+    bad = rec;
+    bad.compensated.begin()->second.begin()->second.pop_back();
+    chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.compensatedProofs && !chk.tally, "short compensated share list flagged");
+    bad = rec;
+    bad.direct["nobody"] = rec.direct.begin()->second;
+    chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.directProofs && !chk.quorum, "unknown guardian flagged");
+    bad = rec;
+    bad.compensated["nobody"] = rec.compensated.begin()->second;
+    chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.recoveryKeys && !chk.compensatedProofs, "unknown missing guardian flagged");
+    bad = rec;
+    bad.counts[0] = -1;
+    chk = verifyDecryptionRecord(G, qb, bad, pks, comm);
+    EXPECT(!chk.tally && chk.directProofs, "negative count flagged");
     // dLogG above the bound -> not found
     EXPECT(!G.dLogG(G.gPowP(G.uIntToElementModQ(1500)), 1000).has_value(), "dLogG beyond maxResult");
   }

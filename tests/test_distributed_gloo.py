@@ -77,3 +77,51 @@ def test_two_rank_tally_fold_equals_global_tally():
         for c in range(2):
             want = G.prodP([int.from_bytes(cts[i, s, c].tobytes(), "big") for i in range(nb)])
             assert int.from_bytes(t[s, c].tobytes(), "big") == want
+
+
+def test_launcher_runs_n_ranks_and_folds_the_global_tally(tmp_path):
+    """bench.py --gpus N without a launcher starts N rank processes through
+    electionguard.launch.run_ranks; the ranks see WORLD_SIZE = N and the folded tally equals
+    the tally over all ballots."""
+    import json
+    import sys
+    from pathlib import Path
+    from electionguard.launch import run_ranks
+    child = Path(__file__).resolve().parent / "_launch_child.py"
+    out = tmp_path / "rank0.json"
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    assert run_ranks(str(child), [str(out)], 2, timeout=240, env=env) == 0
+    d = json.loads(out.read_text())
+    assert d["n_gpus"] == 2 and d["ok"] is True
+    sys.path.insert(0, str(child.parent))
+    import _launch_child as L
+    G = O.production_group()
+    cts = L.ballots(5, 2)
+    for s in range(2):
+        for c in range(2):
+            assert int(d["tally"][s][c], 16) == G.prodP([cts[i][s][c] for i in range(5)])
+
+
+def test_bench_rejects_a_world_size_other_than_gpus():
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_config_names():
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from bench import config_name
+    assert config_name(4, 5, 10_000, 1) == "configs[1]"
+    assert config_name(4, 5, 125_000, 8).startswith("configs[2]")
+    assert config_name(4, 5, 1_000_000, 1).startswith("configs[2]")
+    assert config_name(4, 5, 10_000, 8) == "configs[1] shape (4x5), 10000 ballots per GPU x 8 GPUs"
+    assert config_name(4, 5, 2_000, 2).startswith("configs[1] shape")
+    assert config_name(20, 5, 10_000, 4).startswith("configs[4] shape")

@@ -154,3 +154,35 @@ def test_device_encryption_matches_host(group):
     assert np.array_equal(oc.cpu().numpy(), eb.cts)
     assert np.array_equal(orp.cpu().numpy(), eb.rproof)
     assert np.array_equal(ocp.cpu().numpy(), eb.cproof)
+
+
+def test_host_pointer_encryption_equals_device_resident_with_wide_contests(group):
+    """Two encryption chunks (> 16384 ballots) with a contest of more than 32 selections, so
+    the contest-aggregate product tree runs several rounds through its scratch buffer while
+    chunk 0's outputs are still being copied back (the contest proofs of output
+    set 0 used to share that buffer).  The host-pointer bytes must equal the device-resident
+    encryption's, which has no copy-back overlap."""
+    import torch
+    from electionguard.ballot import (ElectionKey, Manifest, batch_encryption, batch_encryption_device,
+                                      random_scalars, random_votes)
+    from electionguard.keyceremony import key_ceremony
+    man = Manifest(1, 33, 1)          # spc = 34 > 32
+    nb = 16384 + 40
+    gk, K = key_ceremony(group, 2, 2, seed=8)
+    key = ElectionKey(group, K, window_bits=12)
+    rng = np.random.default_rng(8)
+    votes = random_votes(rng, man, nb)
+    sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
+    cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    eb = batch_encryption(group, key, 99, man, votes, sn, cn)
+    dev = torch.device("cuda", 0)
+    dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (votes, sn, cn))
+    oc = torch.empty(eb.cts.shape, dtype=torch.uint8, device=dev)
+    orp = torch.empty(eb.rproof.shape, dtype=torch.uint8, device=dev)
+    ocp = torch.empty(eb.cproof.shape, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    batch_encryption_device(group, key, 99, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
+                            oc.data_ptr(), orp.data_ptr(), ocp.data_ptr())
+    assert np.array_equal(oc.cpu().numpy(), eb.cts)
+    assert np.array_equal(orp.cpu().numpy(), eb.rproof)
+    assert np.array_equal(ocp.cpu().numpy(), eb.cproof)

@@ -82,3 +82,34 @@ def test_tampered_records_fail_their_check(group, election):
     bad.decryption = copy.deepcopy(rec.decryption)
     bad.decryption.counts[3] += 1
     assert _failed(verify_election_record(group, bad)) == ["decryption.tally"]
+
+
+def test_structurally_bad_records_report_false_instead_of_raising(group, election):
+    """empty commitment lists, out-of-range counts, x-coordinates that disagree
+    with the key ceremony, too few available guardians."""
+    from electionguard.record import verify_election_record
+    rec, _ = election
+
+    bad = copy.copy(rec)
+    g0 = copy.deepcopy(rec.guardians[0])
+    g0.commitments, g0.proofs = [], []
+    bad.guardians = [g0] + rec.guardians[1:]
+    res = verify_election_record(group, bad)
+    assert not res["guardian_proofs"] and not res["joint_key"]
+
+    for c in (-1, rec.ballots.n + 1, 2.5):
+        bad = copy.copy(rec)
+        bad.decryption = copy.deepcopy(rec.decryption)
+        bad.decryption.counts[0] = c
+        assert _failed(verify_election_record(group, bad)) == ["decryption.tally"]
+
+    bad = copy.copy(rec)
+    bad.guardians = [copy.deepcopy(g) for g in rec.guardians]
+    bad.guardians[1].x = 9   # the ceremony's x for guardian 2 differs from the record's
+    assert "decryption.quorum" in _failed(verify_election_record(group, bad))
+
+    bad = copy.copy(rec)
+    bad.decryption = copy.deepcopy(rec.decryption)
+    gone = sorted(bad.decryption.direct)[0]
+    del bad.decryption.direct[gone]   # 2 available < quorum 3, and gone is neither available nor missing
+    assert "decryption.quorum" in _failed(verify_election_record(group, bad))

@@ -92,7 +92,13 @@ def main():
         from electionguard.core import constants as C
         co = COracle(C.P, C.Q, C.G)
         s = min(a.cpu_sample, n)
-        thr = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        thr = a.cpu_threads or len(os.sched_getaffinity(0))  # every core this process may use
+        try:  # ... capped by a cgroup CPU quota (more threads than the quota only time-slice)
+            qq = open("/sys/fs/cgroup/cpu.max").read().split()
+            if not a.cpu_threads and qq[0] != "max":
+                thr = max(1, min(thr, int(int(qq[0]) / int(qq[1]) + 0.5)))
+        except (OSError, ValueError, IndexError):
+            pass
         secret = np.frombuffer(int(gk[0].secret).to_bytes(32, "big"), np.uint8)
         from concurrent.futures import ThreadPoolExecutor
 
