@@ -1,0 +1,330 @@
+/* eg_hip_jni.c -- JNI side of electionguard.gpu.EgHip (../java/electionguard/gpu/EgHip.java):
+ * every export of include/eg_hip.h, with array-length checks before any pointer reaches the
+ * library (IllegalArgumentException) and status -> ArithmeticException(eg_last_error()).
+ *
+ * Build (JDK 17; not available in the build container, so not compiled there):
+ *   gcc -O2 -shared -fPIC -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -I include \
+ *       electionguard-remote_amd/jvm/src/main/c/eg_hip_jni.c \
+ *       -L electionguard-remote_amd/electionguard/lib -leg_hip -Wl,-rpath,'$ORIGIN' -o libeg_hip_jni.so
+ *
+ * Host arrays are pinned with Get/ReleasePrimitiveArrayCritical (no copies of batches that can
+ * be hundreds of MB); inputs are released with JNI_ABORT, outputs with 0 (copy back if the VM
+ * copied).  The library call runs inside the critical region: it does not call back into the
+ * VM.  Device pointers (the *Dev methods) are passed through as jlong.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "eg_hip.h"
+
+static void throw_named(JNIEnv* env, const char* cls, const char* msg) {
+  jclass c = (*env)->FindClass(env, cls);
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+static int check_rc(JNIEnv* env, int rc) {
+  if (rc == EG_OK) return 0;
+  throw_named(env, "java/lang/ArithmeticException", eg_last_error());
+  return 1;
+}
+
+/* length check: array a must hold at least `need` bytes (a == NULL allowed when optional) */
+static int need_len(JNIEnv* env, jbyteArray a, size_t need, int optional, const char* what) {
+  if (a == NULL) {
+    if (optional) return 0;
+    throw_named(env, "java/lang/NullPointerException", what);
+    return 1;
+  }
+  if ((size_t)(*env)->GetArrayLength(env, a) < need) {
+    throw_named(env, "java/lang/IllegalArgumentException", what);
+    return 1;
+  }
+  return 0;
+}
+
+#define PIN(a) ((a) ? (uint8_t*)(*env)->GetPrimitiveArrayCritical(env, (a), NULL) : NULL)
+#define UNPIN_IN(a, p) \
+  do { if (a) (*env)->ReleasePrimitiveArrayCritical(env, (a), (p), JNI_ABORT); } while (0)
+#define UNPIN_OUT(a, p) \
+  do { if (a) (*env)->ReleasePrimitiveArrayCritical(env, (a), (p), 0); } while (0)
+
+/* ---------------------------------------------------------------- library / context */
+
+JNIEXPORT jstring JNICALL Java_electionguard_gpu_EgHip_version(JNIEnv* env, jclass cls) {
+  char buf[256];
+  if (check_rc(env, eg_version(buf, sizeof buf))) return NULL;
+  return (*env)->NewStringUTF(env, buf);
+}
+
+JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_ctxCreate(JNIEnv* env, jclass cls, jbyteArray p, jbyteArray q,
+                                                               jbyteArray g, jint device) {
+  if (need_len(env, p, EG_P_BYTES, 0, "p: 512 bytes") || need_len(env, q, EG_Q_BYTES, 0, "q: 32 bytes") ||
+      need_len(env, g, EG_P_BYTES, 0, "g: 512 bytes"))
+    return 0;
+  uint8_t pb[EG_P_BYTES], qb[EG_Q_BYTES], gb[EG_P_BYTES];
+  (*env)->GetByteArrayRegion(env, p, 0, EG_P_BYTES, (jbyte*)pb);
+  (*env)->GetByteArrayRegion(env, q, 0, EG_Q_BYTES, (jbyte*)qb);
+  (*env)->GetByteArrayRegion(env, g, 0, EG_P_BYTES, (jbyte*)gb);
+  eg_ctx* ctx = NULL;
+  if (check_rc(env, eg_ctx_create(pb, qb, gb, device, &ctx))) return 0;
+  return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_ctxDestroy(JNIEnv* env, jclass cls, jlong ctx) {
+  check_rc(env, eg_ctx_destroy((eg_ctx*)(intptr_t)ctx));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_ctxSync(JNIEnv* env, jclass cls, jlong ctx) {
+  check_rc(env, eg_ctx_sync((eg_ctx*)(intptr_t)ctx));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_profileBegin(JNIEnv* env, jclass cls, jlong ctx) {
+  check_rc(env, eg_ctx_profile_begin((eg_ctx*)(intptr_t)ctx));
+}
+
+JNIEXPORT jdoubleArray JNICALL Java_electionguard_gpu_EgHip_profileEnd(JNIEnv* env, jclass cls, jlong ctx) {
+  double v[4] = {0, 0, 0, 0};
+  int launches = 0;
+  if (check_rc(env, eg_ctx_profile_end((eg_ctx*)(intptr_t)ctx, &v[0], &v[1], &v[2], &launches))) return NULL;
+  v[3] = (double)launches;
+  jdoubleArray out = (*env)->NewDoubleArray(env, 4);
+  if (out) (*env)->SetDoubleArrayRegion(env, out, 0, 4, v);
+  return out;
+}
+
+JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_gTable(JNIEnv* env, jclass cls, jlong ctx) {
+  return (jlong)(intptr_t)eg_ctx_g_table((eg_ctx*)(intptr_t)ctx);
+}
+
+/* ---------------------------------------------------------------- fixed-base tables */
+
+JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_fixedBaseCreate(JNIEnv* env, jclass cls, jlong ctx,
+                                                                     jbyteArray base, jint wbits) {
+  if (need_len(env, base, EG_P_BYTES, 0, "base: 512 bytes")) return 0;
+  uint8_t b[EG_P_BYTES];
+  (*env)->GetByteArrayRegion(env, base, 0, EG_P_BYTES, (jbyte*)b);
+  eg_fixed_base* fb = NULL;
+  if (check_rc(env, eg_fixed_base_create((eg_ctx*)(intptr_t)ctx, b, wbits, &fb))) return 0;
+  return (jlong)(intptr_t)fb;
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_fixedBaseDestroy(JNIEnv* env, jclass cls, jlong fb) {
+  check_rc(env, eg_fixed_base_destroy((eg_fixed_base*)(intptr_t)fb));
+}
+
+/* ---------------------------------------------------------------- batched group ops */
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_powpBatch(JNIEnv* env, jclass cls, jlong ctx, jbyteArray bases,
+                                                              jbyteArray exps, jbyteArray out, jint n) {
+  if (n < 0 || need_len(env, bases, (size_t)n * EG_P_BYTES, 0, "bases") ||
+      need_len(env, exps, (size_t)n * EG_Q_BYTES, 0, "exps") || need_len(env, out, (size_t)n * EG_P_BYTES, 0, "out"))
+    return;
+  uint8_t *b = PIN(bases), *e = PIN(exps), *o = PIN(out);
+  const int rc = eg_powp_batch((eg_ctx*)(intptr_t)ctx, b, e, o, (size_t)n);
+  UNPIN_OUT(out, o);
+  UNPIN_IN(exps, e);
+  UNPIN_IN(bases, b);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_fbPowBatch(JNIEnv* env, jclass cls, jlong fb, jbyteArray exps,
+                                                               jbyteArray out, jint n) {
+  if (n < 0 || need_len(env, exps, (size_t)n * EG_Q_BYTES, 0, "exps") ||
+      need_len(env, out, (size_t)n * EG_P_BYTES, 0, "out"))
+    return;
+  uint8_t *e = PIN(exps), *o = PIN(out);
+  const int rc = eg_fb_pow_batch((eg_fixed_base*)(intptr_t)fb, e, o, (size_t)n);
+  UNPIN_OUT(out, o);
+  UNPIN_IN(exps, e);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_powpBatchDev(JNIEnv* env, jclass cls, jlong ctx, jlong dBases,
+                                                                 jlong dExps, jlong dOut, jlong n) {
+  check_rc(env, eg_powp_batch_dev((eg_ctx*)(intptr_t)ctx, (const uint8_t*)(intptr_t)dBases,
+                                  (const uint8_t*)(intptr_t)dExps, (uint8_t*)(intptr_t)dOut, (size_t)n));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_fbPowBatchDev(JNIEnv* env, jclass cls, jlong fb, jlong dExps,
+                                                                  jlong dOut, jlong n) {
+  check_rc(env, eg_fb_pow_batch_dev((eg_fixed_base*)(intptr_t)fb, (const uint8_t*)(intptr_t)dExps,
+                                    (uint8_t*)(intptr_t)dOut, (size_t)n));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_multpBatch(JNIEnv* env, jclass cls, jlong ctx, jbyteArray a,
+                                                               jbyteArray b, jbyteArray out, jint n) {
+  const size_t len = (size_t)n * EG_P_BYTES;
+  if (n < 0 || need_len(env, a, len, 0, "a") || need_len(env, b, len, 0, "b") || need_len(env, out, len, 0, "out"))
+    return;
+  uint8_t *pa = PIN(a), *pb = PIN(b), *o = PIN(out);
+  const int rc = eg_multp_batch((eg_ctx*)(intptr_t)ctx, pa, pb, o, (size_t)n);
+  UNPIN_OUT(out, o);
+  UNPIN_IN(b, pb);
+  UNPIN_IN(a, pa);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_prodReduce(JNIEnv* env, jclass cls, jlong ctx, jbyteArray elems,
+                                                               jint groups, jint len, jbyteArray out) {
+  if (groups < 0 || len < 0 || need_len(env, elems, (size_t)groups * len * EG_P_BYTES, 0, "elems") ||
+      need_len(env, out, (size_t)groups * EG_P_BYTES, 0, "out"))
+    return;
+  uint8_t *e = PIN(elems), *o = PIN(out);
+  const int rc = eg_prod_reduce((eg_ctx*)(intptr_t)ctx, e, (size_t)groups, (size_t)len, o);
+  UNPIN_OUT(out, o);
+  UNPIN_IN(elems, e);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_multinvBatch(JNIEnv* env, jclass cls, jlong ctx, jbyteArray a,
+                                                                 jbyteArray out, jint n) {
+  const size_t len = (size_t)n * EG_P_BYTES;
+  if (n < 0 || need_len(env, a, len, 0, "a") || need_len(env, out, len, 0, "out")) return;
+  uint8_t *pa = PIN(a), *o = PIN(out);
+  const int rc = eg_multinv_batch((eg_ctx*)(intptr_t)ctx, pa, o, (size_t)n);
+  UNPIN_OUT(out, o);
+  UNPIN_IN(a, pa);
+  check_rc(env, rc);
+}
+
+/* ---------------------------------------------------------------- ballots */
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_verifyBallots(JNIEnv* env, jclass cls, jlong ctx, jbyteArray K,
+                                                                  jbyteArray qbar, jint nb, jint nc, jint spc,
+                                                                  jint ph, jint limit, jbyteArray cts,
+                                                                  jbyteArray rproof, jbyteArray cproof,
+                                                                  jbyteArray okSel, jbyteArray okCon,
+                                                                  jbyteArray tally) {
+  if (nb < 0 || nc <= 0 || spc <= 0 || ph < 0 || ph >= spc) {
+    throw_named(env, "java/lang/IllegalArgumentException", "bad manifest shape");
+    return;
+  }
+  const size_t nsel = (size_t)nc * spc, nreal = (size_t)nc * (spc - ph);
+  if (need_len(env, K, EG_P_BYTES, 0, "K") || need_len(env, qbar, EG_Q_BYTES, 0, "qbar") ||
+      need_len(env, cts, (size_t)nb * nsel * 1024, 0, "cts") || need_len(env, rproof, (size_t)nb * nsel * 128, 0, "rproof") ||
+      need_len(env, cproof, (size_t)nb * nc * 64, 0, "cproof") || need_len(env, okSel, (size_t)nb * nsel, 0, "okSel") ||
+      need_len(env, okCon, (size_t)nb * nc, 0, "okContest") || need_len(env, tally, nreal * 2 * EG_P_BYTES, 1, "tally"))
+    return;
+  uint8_t kb[EG_P_BYTES], qb[EG_Q_BYTES];
+  (*env)->GetByteArrayRegion(env, K, 0, EG_P_BYTES, (jbyte*)kb);
+  (*env)->GetByteArrayRegion(env, qbar, 0, EG_Q_BYTES, (jbyte*)qb);
+  uint8_t *c = PIN(cts), *r = PIN(rproof), *p = PIN(cproof), *os = PIN(okSel), *oc = PIN(okCon), *t = PIN(tally);
+  const int rc = eg_verify_ballots((eg_ctx*)(intptr_t)ctx, kb, qb, (size_t)nb, (size_t)nc, (size_t)spc, (size_t)ph,
+                                   (uint32_t)limit, c, r, p, os, oc, t);
+  UNPIN_OUT(tally, t);
+  UNPIN_OUT(okCon, oc);
+  UNPIN_OUT(okSel, os);
+  UNPIN_IN(cproof, p);
+  UNPIN_IN(rproof, r);
+  UNPIN_IN(cts, c);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_setElectionKey(JNIEnv* env, jclass cls, jlong ctx, jbyteArray K,
+                                                                   jint wbits) {
+  if (need_len(env, K, EG_P_BYTES, 0, "K")) return;
+  uint8_t kb[EG_P_BYTES];
+  (*env)->GetByteArrayRegion(env, K, 0, EG_P_BYTES, (jbyte*)kb);
+  check_rc(env, eg_set_election_key((eg_ctx*)(intptr_t)ctx, kb, wbits));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_verifyBallotsDev(JNIEnv* env, jclass cls, jlong ctx,
+                                                                     jbyteArray qbar, jlong nb, jlong nc, jlong spc,
+                                                                     jlong ph, jint limit, jlong dCts, jlong dRproof,
+                                                                     jlong dCproof, jlong dOkSel, jlong dOkCon,
+                                                                     jlong dTally) {
+  if (need_len(env, qbar, EG_Q_BYTES, 0, "qbar")) return;
+  uint8_t qb[EG_Q_BYTES];
+  (*env)->GetByteArrayRegion(env, qbar, 0, EG_Q_BYTES, (jbyte*)qb);
+  check_rc(env, eg_verify_ballots_dev((eg_ctx*)(intptr_t)ctx, qb, (size_t)nb, (size_t)nc, (size_t)spc, (size_t)ph,
+                                      (uint32_t)limit, (const uint8_t*)(intptr_t)dCts,
+                                      (const uint8_t*)(intptr_t)dRproof, (const uint8_t*)(intptr_t)dCproof,
+                                      (uint8_t*)(intptr_t)dOkSel, (uint8_t*)(intptr_t)dOkCon,
+                                      (uint8_t*)(intptr_t)dTally));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_encryptBallots(JNIEnv* env, jclass cls, jlong ctx,
+                                                                   jbyteArray qbar, jint nb, jint nc, jint spc,
+                                                                   jbyteArray votes, jbyteArray selNonces,
+                                                                   jbyteArray conNonces, jbyteArray cts,
+                                                                   jbyteArray rproof, jbyteArray cproof) {
+  if (nb < 0 || nc <= 0 || spc <= 0) {
+    throw_named(env, "java/lang/IllegalArgumentException", "bad manifest shape");
+    return;
+  }
+  const size_t nsel = (size_t)nc * spc;
+  if (need_len(env, qbar, EG_Q_BYTES, 0, "qbar") || need_len(env, votes, (size_t)nb * nsel, 0, "votes") ||
+      need_len(env, selNonces, (size_t)nb * nsel * 128, 0, "selNonces") ||
+      need_len(env, conNonces, (size_t)nb * nc * 32, 0, "contestNonces") ||
+      need_len(env, cts, (size_t)nb * nsel * 1024, 0, "cts") || need_len(env, rproof, (size_t)nb * nsel * 128, 0, "rproof") ||
+      need_len(env, cproof, (size_t)nb * nc * 64, 0, "cproof"))
+    return;
+  uint8_t qb[EG_Q_BYTES];
+  (*env)->GetByteArrayRegion(env, qbar, 0, EG_Q_BYTES, (jbyte*)qb);
+  uint8_t *v = PIN(votes), *sn = PIN(selNonces), *cn = PIN(conNonces), *c = PIN(cts), *r = PIN(rproof), *p = PIN(cproof);
+  const int rc = eg_encrypt_ballots((eg_ctx*)(intptr_t)ctx, qb, (size_t)nb, (size_t)nc, (size_t)spc, v, sn, cn, c, r, p);
+  UNPIN_OUT(cproof, p);
+  UNPIN_OUT(rproof, r);
+  UNPIN_OUT(cts, c);
+  UNPIN_IN(conNonces, cn);
+  UNPIN_IN(selNonces, sn);
+  UNPIN_IN(votes, v);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_encryptBallotsDev(JNIEnv* env, jclass cls, jlong ctx,
+                                                                      jbyteArray qbar, jlong nb, jlong nc, jlong spc,
+                                                                      jlong dVotes, jlong dSelNonces,
+                                                                      jlong dConNonces, jlong dCts, jlong dRproof,
+                                                                      jlong dCproof) {
+  if (need_len(env, qbar, EG_Q_BYTES, 0, "qbar")) return;
+  uint8_t qb[EG_Q_BYTES];
+  (*env)->GetByteArrayRegion(env, qbar, 0, EG_Q_BYTES, (jbyte*)qb);
+  check_rc(env, eg_encrypt_ballots_dev((eg_ctx*)(intptr_t)ctx, qb, (size_t)nb, (size_t)nc, (size_t)spc,
+                                       (const uint8_t*)(intptr_t)dVotes, (const uint8_t*)(intptr_t)dSelNonces,
+                                       (const uint8_t*)(intptr_t)dConNonces, (uint8_t*)(intptr_t)dCts,
+                                       (uint8_t*)(intptr_t)dRproof, (uint8_t*)(intptr_t)dCproof));
+}
+
+/* ---------------------------------------------------------------- trustee */
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_trusteeDecryptBatch(JNIEnv* env, jclass cls, jlong ctx,
+                                                                        jbyteArray secret, jbyteArray qbar,
+                                                                        jbyteArray texts, jbyteArray nonces, jint n,
+                                                                        jbyteArray outM, jbyteArray outProof) {
+  if (n < 0 || need_len(env, secret, EG_Q_BYTES, 0, "secret") || need_len(env, qbar, EG_Q_BYTES, 0, "qbar") ||
+      need_len(env, texts, (size_t)n * 1024, 0, "texts") || need_len(env, nonces, (size_t)n * 32, 0, "nonces") ||
+      need_len(env, outM, (size_t)n * EG_P_BYTES, 0, "outM") || need_len(env, outProof, (size_t)n * 64, 0, "outProof"))
+    return;
+  uint8_t sb[EG_Q_BYTES], qb[EG_Q_BYTES];
+  (*env)->GetByteArrayRegion(env, secret, 0, EG_Q_BYTES, (jbyte*)sb);
+  (*env)->GetByteArrayRegion(env, qbar, 0, EG_Q_BYTES, (jbyte*)qb);
+  uint8_t *t = PIN(texts), *u = PIN(nonces), *m = PIN(outM), *pr = PIN(outProof);
+  const int rc = eg_trustee_decrypt_batch((eg_ctx*)(intptr_t)ctx, sb, qb, t, u, (size_t)n, m, pr);
+  UNPIN_OUT(outProof, pr);
+  UNPIN_OUT(outM, m);
+  UNPIN_IN(nonces, u);
+  UNPIN_IN(texts, t);
+  memset(sb, 0, sizeof sb); /* the secret share leaves no copy on this stack frame */
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_verifyShares(JNIEnv* env, jclass cls, jlong ctx, jbyteArray qbar,
+                                                                 jbyteArray Ki, jbyteArray texts, jbyteArray M,
+                                                                 jbyteArray proof, jint n, jbyteArray ok) {
+  if (n < 0 || need_len(env, qbar, EG_Q_BYTES, 0, "qbar") || need_len(env, Ki, (size_t)n * EG_P_BYTES, 0, "Ki") ||
+      need_len(env, texts, (size_t)n * 1024, 0, "texts") || need_len(env, M, (size_t)n * EG_P_BYTES, 0, "M") ||
+      need_len(env, proof, (size_t)n * 64, 0, "proof") || need_len(env, ok, (size_t)n, 0, "ok"))
+    return;
+  uint8_t qb[EG_Q_BYTES];
+  (*env)->GetByteArrayRegion(env, qbar, 0, EG_Q_BYTES, (jbyte*)qb);
+  uint8_t *k = PIN(Ki), *t = PIN(texts), *m = PIN(M), *p = PIN(proof), *o = PIN(ok);
+  const int rc = eg_verify_shares((eg_ctx*)(intptr_t)ctx, qb, k, t, m, p, (size_t)n, o);
+  UNPIN_OUT(ok, o);
+  UNPIN_IN(proof, p);
+  UNPIN_IN(M, m);
+  UNPIN_IN(texts, t);
+  UNPIN_IN(Ki, k);
+  check_rc(env, rc);
+}

@@ -1,0 +1,94 @@
+package electionguard.gpu;
+
+/**
+ * JNI binding of libeg_hip.so: one native method per export of include/eg_hip.h (the C ABI
+ * of the MI355X path).  Native side: ../c/eg_hip_jni.c (build: see INTEGRATION.md §2).
+ *
+ * Conventions (the reference's wire layout, src/main/proto/common.proto:6-16):
+ *   - element arrays are n fixed-width big-endian values concatenated: ElementModP 512 B,
+ *     ElementModQ 32 B, ElGamalCiphertext (pad, data) 1024 B;
+ *   - {@code long} handles are eg_ctx* / eg_fixed_base*; {@code long} d* arguments of the *Dev
+ *     methods are device (HBM) pointers, e.g. from another native HIP allocation;
+ *   - a non-zero status throws {@link ArithmeticException} with eg_last_error(), the mapping the
+ *     reference's callers expect from upstream arithmetic (RunRemoteDecryptingTrustee.java:200-204
+ *     turns any Throwable into the RPC's error string).
+ *
+ * JDK 17 target (.idea/misc.xml:3): JNI, not Panama FFM (FFM is final only from JDK 22).
+ * No JDK exists in the build container, so this file and the C side are not compiled there.
+ */
+public final class EgHip {
+  static {
+    System.loadLibrary("eg_hip_jni"); // links libeg_hip.so (rpath / LD_LIBRARY_PATH)
+  }
+
+  private EgHip() {}
+
+  public static final int P_BYTES = 512;
+  public static final int Q_BYTES = 32;
+
+  // ---- library / context (KUtils.productionGroup, KUtils.java:10-12) ----
+  public static native String version();
+
+  public static native long ctxCreate(byte[] p512, byte[] q32, byte[] g512, int device);
+
+  public static native void ctxDestroy(long ctx);
+
+  public static native void ctxSync(long ctx);
+
+  public static native void profileBegin(long ctx);
+
+  /** @return {kernel ms, Montgomery ops, of which squarings, launches} of the dominant kernel. */
+  public static native double[] profileEnd(long ctx);
+
+  /** The fixed-base table of g built at ctxCreate (owned by the context: do not destroy). */
+  public static native long gTable(long ctx);
+
+  // ---- fixed-base tables (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit windows) ----
+  public static native long fixedBaseCreate(long ctx, byte[] base512, int windowBits);
+
+  public static native void fixedBaseDestroy(long fb);
+
+  // ---- batched group ops: ElementModP.powP / gPowP / times / multP() / multInv ----
+  public static native void powpBatch(long ctx, byte[] bases, byte[] exps, byte[] out, int n);
+
+  public static native void fbPowBatch(long fb, byte[] exps, byte[] out, int n);
+
+  public static native void powpBatchDev(long ctx, long dBases, long dExps, long dOut, long n);
+
+  public static native void fbPowBatchDev(long fb, long dExps, long dOut, long n);
+
+  public static native void multpBatch(long ctx, byte[] a, byte[] b, byte[] out, int n);
+
+  /** out[g] = prod_k elems[g*len + k] (Iterable<ElementModP>.multP(); runAccumulateBallots). */
+  public static native void prodReduce(long ctx, byte[] elems, int groups, int len, byte[] out);
+
+  public static native void multinvBatch(long ctx, byte[] a, byte[] out, int n);
+
+  // ---- ballots: Verifier(record, 11).verify() + runAccumulateBallots, batchEncryption ----
+  // (RunRemoteWorkflowTest.java:140-141,151,179-182).  Layouts: include/eg_hip.h.
+  public static native void verifyBallots(long ctx, byte[] K512, byte[] qbar32, int nb, int nc, int spc,
+                                          int placeholders, int limit, byte[] cts, byte[] rproof, byte[] cproof,
+                                          byte[] okSel, byte[] okContest, byte[] tally);
+
+  public static native void setElectionKey(long ctx, byte[] K512, int windowBits);
+
+  public static native void verifyBallotsDev(long ctx, byte[] qbar32, long nb, long nc, long spc, long placeholders,
+                                             int limit, long dCts, long dRproof, long dCproof, long dOkSel,
+                                             long dOkContest, long dTally);
+
+  public static native void encryptBallots(long ctx, byte[] qbar32, int nb, int nc, int spc, byte[] votes,
+                                           byte[] selNonces, byte[] contestNonces, byte[] cts, byte[] rproof,
+                                           byte[] cproof);
+
+  public static native void encryptBallotsDev(long ctx, byte[] qbar32, long nb, long nc, long spc, long dVotes,
+                                              long dSelNonces, long dContestNonces, long dCts, long dRproof,
+                                              long dCproof);
+
+  // ---- trustee (DecryptingTrusteeIF, RunRemoteDecryptingTrustee.java:189-193,227-232) ----
+  public static native void trusteeDecryptBatch(long ctx, byte[] secret32, byte[] qbar32, byte[] texts, byte[] nonces,
+                                                int n, byte[] outM, byte[] outProof);
+
+  /** Mediator side of Decryption.decrypt (RunRemoteDecryptor.java:261-262): share-proof checks. */
+  public static native void verifyShares(long ctx, byte[] qbar32, byte[] Ki, byte[] texts, byte[] M, byte[] proof,
+                                         int n, byte[] ok);
+}
