@@ -141,10 +141,9 @@ class DecryptingTrusteeServer:
                 self._finish, request_deserializer=MSG["FinishRequest"].FromString,
                 response_serializer=MSG["ErrorResponse"].SerializeToString),
         }
-        # default 4 MiB inbound cap as the reference channel; raise for large tallies
-        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
-                                  options=[("grpc.max_receive_message_length", 256 << 20),
-                                           ("grpc.max_send_message_length", 256 << 20)])
+        # gRPC's default limits, as the reference's server (RunRemoteDecryptingTrustee.java:111-112):
+        # 4 MiB inbound; RemoteDecryptingTrusteeProxy keeps every request and response below it
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers))
         self.server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
         self.port = self.server.add_insecure_port(f"{host}:{port}")
 
@@ -199,16 +198,27 @@ class DecryptingTrusteeServer:
         return MSG["ErrorResponse"]()
 
 
-class RemoteDecryptingTrusteeProxy:
-    """Mediator-side DecryptingTrusteeIF over gRPC (RemoteDecryptingTrusteeProxy.java)."""
+# Texts per RPC so that every message stays under gRPC's default 4 MiB inbound limit on both
+# ends: a request text is ~1,039 B on the wire, a compensated result ~1,112 B (M, proof, recovery
+# key), so 3,500 texts are ~3.9 MB.  The reference sends the whole tally in one RPC
+# (RemoteDecryptingTrusteeProxy.java:55-63), which its default channels reject above ~3.8k texts.
+MAX_TEXTS_PER_RPC = 3500
 
-    def __init__(self, trustee_id: str, url: str, x: int, public_key: int):
+
+class RemoteDecryptingTrusteeProxy:
+    """Mediator-side DecryptingTrusteeIF over gRPC (RemoteDecryptingTrusteeProxy.java).  A call
+    over more than ``max_texts_per_rpc`` texts is split into consecutive RPCs whose results are
+    concatenated in text order; if any of them fails the call returns [] (:64-66, :103-105)."""
+
+    def __init__(self, trustee_id: str, url: str, x: int, public_key: int,
+                 max_texts_per_rpc: int = MAX_TEXTS_PER_RPC):
         import grpc
 
         self._id, self._x, self._K = trustee_id, x, public_key
-        self.channel = grpc.insecure_channel(url, options=[("grpc.max_receive_message_length", 256 << 20),
-                                                           ("grpc.max_send_message_length", 256 << 20),
-                                                           ("grpc.keepalive_time_ms", 60000)])
+        self.max_texts = max_texts_per_rpc
+        # default message limits (4 MiB inbound) and the reference's 1-minute keepalive
+        # (RemoteDecryptingTrusteeProxy.java:202-210)
+        self.channel = grpc.insecure_channel(url, options=[("grpc.keepalive_time_ms", 60000)])
         mk = lambda m, req, resp: self.channel.unary_unary(f"/{SERVICE}/{m}", request_serializer=req.SerializeToString,
                                                            response_deserializer=resp.FromString)
         self._direct = mk("directDecrypt", MSG["DirectDecryptionRequest"], MSG["DirectDecryptionResponse"])
@@ -224,47 +234,56 @@ class RemoteDecryptingTrusteeProxy:
     def electionPublicKey(self) -> int:
         return self._K
 
-    def directDecrypt(self, group, texts, extendedBaseHash: int, nonce=None):
-        import grpc
-        from .decrypt import DirectDecryptionAndProof, GenericChaumPedersenProof, _texts_array
+    def _batches(self, texts):
+        from .decrypt import _texts_array
 
         T = _texts_array(texts)
-        req = MSG["DirectDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash),
-                                             text=[publish_ct(int.from_bytes(t[0].tobytes(), "big"),
-                                                              int.from_bytes(t[1].tobytes(), "big")) for t in T])
-        try:
-            resp = self._direct(req)
-        except grpc.RpcError as e:
-            log.error("directDecrypt failed: %s", e)
-            return []
-        if resp.error:
-            log.error("directDecrypt failed: %s", resp.error)
+        for a in range(0, len(T), self.max_texts):
+            yield [publish_ct(int.from_bytes(t[0].tobytes(), "big"), int.from_bytes(t[1].tobytes(), "big"))
+                   for t in T[a:a + self.max_texts]]
+
+    def _call(self, name, stub, requests):
+        import grpc
+
+        results = []
+        for req in requests:
+            try:
+                resp = stub(req)
+            except grpc.RpcError as e:
+                log.error("%s failed: %s", name, e)
+                return None
+            if resp.error:
+                log.error("%s failed: %s", name, resp.error)
+                return None
+            results.extend(resp.results)
+        return results
+
+    def directDecrypt(self, group, texts, extendedBaseHash: int, nonce=None):
+        from .decrypt import DirectDecryptionAndProof, GenericChaumPedersenProof
+
+        reqs = (MSG["DirectDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash), text=b)
+                for b in self._batches(texts))
+        res = self._call("directDecrypt", self._direct, reqs)
+        if res is None:
             return []
         return [DirectDecryptionAndProof(import_int(r.decryption),
                                          GenericChaumPedersenProof(import_int(r.proof.challenge),
                                                                    import_int(r.proof.response)))
-                for r in resp.results]
+                for r in res]
 
     def compensatedDecrypt(self, group, missingGuardianId: str, texts, extendedBaseHash: int, nonce=None):
-        import grpc
-        from .decrypt import CompensatedDecryptionAndProof, GenericChaumPedersenProof, _texts_array
+        from .decrypt import CompensatedDecryptionAndProof, GenericChaumPedersenProof
 
-        T = _texts_array(texts)
-        req = MSG["CompensatedDecryptionRequest"](
-            extended_base_hash=publish_q(extendedBaseHash), missing_guardian_id=missingGuardianId,
-            text=[publish_ct(int.from_bytes(t[0].tobytes(), "big"), int.from_bytes(t[1].tobytes(), "big")) for t in T])
-        try:
-            resp = self._comp(req)
-        except grpc.RpcError as e:
-            log.error("compensatedDecrypt failed: %s", e)
-            return []
-        if resp.error:
-            log.error("compensatedDecrypt failed: %s", resp.error)
+        reqs = (MSG["CompensatedDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash),
+                                                     missing_guardian_id=missingGuardianId, text=b)
+                for b in self._batches(texts))
+        res = self._call("compensatedDecrypt", self._comp, reqs)
+        if res is None:
             return []
         return [CompensatedDecryptionAndProof(import_int(r.decryption),
                                               GenericChaumPedersenProof(import_int(r.proof.challenge),
                                                                         import_int(r.proof.response)),
-                                              import_int(r.recoveryPublicKey)) for r in resp.results]
+                                              import_int(r.recoveryPublicKey)) for r in res]
 
     def finish(self, all_ok: bool) -> str:
         import grpc

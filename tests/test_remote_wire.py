@@ -85,3 +85,50 @@ def test_proxy_transport_failure_returns_empty(setup):
     px = RemoteDecryptingTrusteeProxy("x", "127.0.0.1:1", 1, 1)
     assert px.directDecrypt(None, [(texts[0].pad, texts[0].data)], qbar) == []
     px.close()
+
+
+class EchoTrustee:
+    """Stand-in whose results are cheap functions of the texts (wire sizing test only): M = pad,
+    proof (c, v) = (i, data mod q), recovery key = data.  Records the batch sizes it served."""
+
+    def __init__(self, q):
+        self.q, self.calls = q, []
+
+    def directDecrypt(self, group, texts, qbar, nonce=None):
+        from electionguard.decrypt import DirectDecryptionAndProof, GenericChaumPedersenProof
+        self.calls.append(len(texts))
+        return [DirectDecryptionAndProof(a, GenericChaumPedersenProof(qbar, b % self.q)) for a, b in texts]
+
+    def compensatedDecrypt(self, group, missing_id, texts, qbar, nonce=None):
+        from electionguard.decrypt import CompensatedDecryptionAndProof, GenericChaumPedersenProof
+        self.calls.append(len(texts))
+        return [CompensatedDecryptionAndProof(a, GenericChaumPedersenProof(qbar, b % self.q), b) for a, b in texts]
+
+
+def test_ten_thousand_texts_fit_default_channel_limits():
+    """A 10k-text tally through default-limit channels (4 MiB inbound on both ends, as the
+    reference's RemoteDecryptingTrusteeProxy.java:202-210 and its server): the proxy splits it
+    into <= 3,500-text RPCs and reassembles the results in text order."""
+    from electionguard.remote import MAX_TEXTS_PER_RPC, DecryptingTrusteeServer, RemoteDecryptingTrusteeProxy
+    G = O.production_group()
+    rng = random.Random(4)
+    n = 10_000
+    texts = [(rng.randrange(G.p), rng.randrange(G.p)) for _ in range(n)]
+    tr = EchoTrustee(G.q)
+    srv = DecryptingTrusteeServer(None, tr).start()
+    try:
+        px = RemoteDecryptingTrusteeProxy("g1", f"127.0.0.1:{srv.port}", 1, 1)
+        res = px.directDecrypt(None, texts, 77)
+        assert len(res) == n and tr.calls == [3500, 3500, 3000] and MAX_TEXTS_PER_RPC == 3500
+        assert all(r.partialDecryption == a and r.proof.v == b % G.q for r, (a, b) in zip(res, texts))
+        tr.calls.clear()
+        cres = px.compensatedDecrypt(None, "g2", texts, 77)
+        assert len(cres) == n and tr.calls == [3500, 3500, 3000]
+        assert all(r.recoveredPublicKeyShare == b for r, (a, b) in zip(cres, texts))
+        # one RPC of the whole tally, as the reference sends it, exceeds the default limit
+        big = RemoteDecryptingTrusteeProxy("g1", f"127.0.0.1:{srv.port}", 1, 1, max_texts_per_rpc=n)
+        assert big.directDecrypt(None, texts, 77) == []
+        big.close()
+        px.close()
+    finally:
+        srv.stop()
