@@ -139,6 +139,7 @@ struct eg_ctx {
   uint8_t* d_qbar = nullptr;
   eg_fixed_base* gtab = nullptr;
   eg_fixed_base* Ktab = nullptr;
+  uint32_t* d_gcomb = nullptr;  // Lim-Lee comb subset table of g (32 elements) for constant-time g^u
   DevBuf ws[W_NSLOT];
   bool timing = false;
   std::vector<ProfRec> prof;
@@ -202,7 +203,7 @@ struct MMCount {
 };
 static MMCount pow_job_mm(const MontConsts& H, const PowShape& S, const FbTab& f0, const FbTab& f1) {
   MMCount n;
-  if (S.has_base) {
+  if (S.has_base && !(S.comb && S.shared_comb)) {
     if (S.comb) {
       if (S.gather)
         n.mul += (double)((kCombH - 1) * (S.gather - 1));  // y_k gathered from the factors' y_k
@@ -254,12 +255,18 @@ struct PowTail {
   const uint32_t* ygat;
 };
 static size_t pow_scratch_per_group(const PowShape& S) {
-  return S.has_base ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
+  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
 }
+// ct = true: the constant-time instantiation k_pow<F, true> for secret exponents (comb shapes
+// without fixed-base terms only); ctab: the shared comb table of S.shared_comb jobs.
 static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
                       const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1, uint32_t* yout = nullptr,
-                      const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr) {
+                      const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr,
+                      bool ct = false, const uint32_t* ctab = nullptr) {
   if (S.resid && (!S.comb || S.gather || !rout)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
+  if (S.shared_comb && (!S.comb || S.gather || S.resid || !ctab)) return fail(EG_ERR_ARG, "shared comb table missing");
+  if (ct && (!S.has_base || !S.comb || S.gather || S.nfb[0] || S.nfb[1] || tail))
+    return fail(EG_ERR_ARG, "constant-time jobs are plain comb shapes without fixed-base terms");
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
   if (tail && tail->S.gather && (!tail->S.comb || !tail->ygat))
     return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
@@ -280,11 +287,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
     if (rc) return rc;
     PowPart P0{S, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
-               yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat, rout ? rout + off * 2 * kW : nullptr};
+               yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat, rout ? rout + off * 2 * kW : nullptr, ctab};
     PowPart P1{};
     if (nt) {
       P1 = PowPart{tail->S, tail->jobs, (uint32_t)nt, grid_for(nt),
-                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, nullptr};
+                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, nullptr, nullptr};
     }
     ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
@@ -293,7 +300,14 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
       HIPCHK(hipEventCreate(&pr.b));
       HIPCHK(hipEventRecord(pr.a, c->stream));
     }
-    LAUNCH_F(c, k_pow, dim3(P0.nblocks + P1.nblocks), c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+    const dim3 grid(P0.nblocks + P1.nblocks);
+    if (c->h.friendly) {
+      if (ct) hipLaunchKernelGGL((k_pow<true, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+      else hipLaunchKernelGGL((k_pow<true, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+    } else {
+      if (ct) hipLaunchKernelGGL((k_pow<false, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+      else hipLaunchKernelGGL((k_pow<false, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+    }
     HIPCHK(hipGetLastError());
     if (c->timing) {
       HIPCHK(hipEventRecord(pr.b, c->stream));
@@ -497,6 +511,7 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);
+  if (c->d_gcomb) hipFree(c->d_gcomb);
   if (c->copy) {
     hipStreamSynchronize(c->copy);
     hipStreamDestroy(c->copy);

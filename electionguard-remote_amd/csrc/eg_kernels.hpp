@@ -295,7 +295,35 @@ struct PowShape {
   uint32_t resid;      // comb jobs (not gather): also write the residue-test pair of the base B,
                        // z = B^(2^256) (48 squarings past y_4) and w = B^c, c = 2^256 - q, to
                        // rout[2 gid], rout[2 gid + 1]; B^q == 1 iff z == w and B != 0 (k_resid_check)
+  uint32_t shared_comb;  // comb jobs whose 32-entry subset table is PowPart::ctab (one table for every
+                         // job, e.g. the trustee's g^u): no per-job precompute
 };
+
+// Constant-time table read for secret digits (k_pow<F, CT = true>, the trustee's shares):
+// every entry of the table is read and the wanted one kept with a mask, so the addresses a
+// job touches do not depend on the digit d.  Each lane selects its own 20-word block.
+__device__ __forceinline__ void ct_select_to_lds(uint32_t* __restrict__ slot, const uint32_t* __restrict__ tbl,
+                                                 int nent, uint32_t d) {
+  const int o = glane() * kLP;
+  uint4 acc[kLP / 4];
+#pragma unroll
+  for (int j = 0; j < kLP / 4; ++j) acc[j] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 1
+  for (int e = 0; e < nent; ++e) {
+    const uint32_t m = 0u - (uint32_t)((uint32_t)e == d);
+    const uint4* src = reinterpret_cast<const uint4*>(tbl + (size_t)e * kW + o);
+#pragma unroll
+    for (int j = 0; j < kLP / 4; ++j) {
+      const uint4 v = src[j];
+      acc[j].x |= v.x & m;
+      acc[j].y |= v.y & m;
+      acc[j].z |= v.z & m;
+      acc[j].w |= v.w & m;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kLP / 4; ++j) *reinterpret_cast<uint4*>(slot + o + 4 * j) = acc[j];
+}
 
 // Lim-Lee comb parameters for 256-bit exponents: 5 rows of 52 bits.
 constexpr int kCombH = 5;
@@ -342,9 +370,14 @@ struct PowPart {
   uint32_t* yout;     // comb y_1..y_4 per job (optional)
   const uint32_t* ygat;  // gather source (S.gather > 0)
   uint32_t* rout;        // residue-test pairs (S.resid), 2 device elements per job
+  const uint32_t* ctab;  // shared comb subset table (S.shared_comb), 32 device elements
 };
 
-template <bool F>
+// CT = true: the constant-time instantiation for secret exponents (trustee shares s_i and
+// P_l(x_i), proof nonces u).  Comb shapes only (no 4-bit window, no radix fixed-base terms):
+// every comb-table read is ct_select_to_lds over all 32 entries, and the square/multiply
+// schedule is the comb's fixed one, so neither time nor addresses depend on exponent bits.
+template <bool F, bool CT>
 __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowPart P0,
                                                 PowPart P1, const uint32_t* __restrict__ elems,
                                                 const uint8_t* __restrict__ scalars,
@@ -368,8 +401,9 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   uint32_t x[kL];
   const bool comb = S.comb != 0;
   const uint32_t tsize = comb ? (1u << kCombH) : 16u;
-  uint32_t* tbl = scratch + (size_t)gid * tsize * kW;
-  const uint32_t* B = S.has_base ? elems + (size_t)J[0] * kW : nullptr;
+  // shared comb table (read-only: its precompute phases are skipped) or the job's scratch table
+  uint32_t* tbl = (comb && S.shared_comb) ? const_cast<uint32_t*>(P.ctab) : scratch + (size_t)gid * tsize * kW;
+  const uint32_t* B = (S.has_base && !S.shared_comb) ? elems + (size_t)J[0] * kW : nullptr;
   const int nwin = (int)S.exp_bytes * 2;
 
   // The whole job is one stream of Montgomery multiplies x <- x * Y driven by a small
@@ -390,7 +424,9 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   uint32_t o = 0, t = 0, kf = 0;
   bool x_is_one = true;
   const uint8_t* e = nullptr;
-  if (S.has_base) {
+  if (S.has_base && comb && S.shared_comb) {
+    phase = kBegin;  // the table is ready
+  } else if (S.has_base) {
     uint32_t one[kL];
     load_elem(one, C->one);
     store_elem(tbl, one);
@@ -479,7 +515,14 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
               dig[j] = (uint8_t)d;
             }
             wave_sync();
-            load_elem(x, tbl + (size_t)dig[kCombW - 1] * kW);
+            if constexpr (CT) {
+              ct_select_to_lds(slot, tbl, 1 << kCombH, dig[kCombW - 1]);
+              wave_sync();
+              load_elem(x, slot);
+              wave_sync();
+            } else {
+              load_elem(x, tbl + (size_t)dig[kCombW - 1] * kW);
+            }
             w = kCombW - 2; sub = 0;
             phase = kComb;
           } else {
@@ -527,7 +570,12 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     if (done) break;
     // ---- the one Montgomery multiply (or square) ----
     if (ysrc) {
-      elem_to_lds(slot, ysrc);
+      if constexpr (CT) {
+        if (phase == kComb) ct_select_to_lds(slot, tbl, 1 << kCombH, dig[w]);  // secret digit
+        else elem_to_lds(slot, ysrc);
+      } else {
+        elem_to_lds(slot, ysrc);
+      }
       wave_sync();
       M.mul(x, slot);
     } else {
@@ -655,11 +703,22 @@ __device__ __forceinline__ void st256(uint8_t* __restrict__ be, const U256& a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) d[7 - i] = __builtin_bswap32(a.w[i]);
 }
+// The mod-q helpers below are branch-free in their operands (trustee responses v = u - c s and
+// the encryption's R c_fake touch secrets): a < b is the borrow of a - b, selections are masks.
 __device__ __forceinline__ bool lt256(const U256& a, const U256& b) {
-  for (int i = 7; i >= 0; --i) {
-    if (a.w[i] != b.w[i]) return a.w[i] < b.w[i];
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (int64_t)a.w[i] - (int64_t)b.w[i];
+    c >>= 32;
   }
-  return false;
+  return c != 0;
+}
+__device__ __forceinline__ U256 sel256(uint32_t mask, const U256& a, const U256& b) {  // mask ? a : b
+  U256 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.w[i] = (a.w[i] & mask) | (b.w[i] & ~mask);
+  return r;
 }
 __device__ __forceinline__ uint32_t add256(U256& a, const U256& b) {
   uint64_t c = 0;
@@ -684,8 +743,9 @@ __device__ __forceinline__ uint32_t sub256(U256& a, const U256& b) {
 // (a + b) mod q for a, b < q
 __device__ __forceinline__ U256 addmod256(U256 a, const U256& b, const U256& q) {
   const uint32_t carry = add256(a, b);
-  if (carry || !lt256(a, q)) sub256(a, q);
-  return a;
+  U256 t = a;
+  const uint32_t borrow = sub256(t, q);
+  return sel256(0u - (carry | (borrow ^ 1u)), t, a);  // subtract q iff a + b >= q
 }
 // (L * a) mod q for a < q, L < 2^32  (schoolbook + repeated subtraction-free fold)
 __device__ __forceinline__ U256 mulsmall_mod(const U256& a, uint32_t L, const U256& q) {
@@ -720,16 +780,20 @@ __device__ __forceinline__ U256 negmod(const U256& a, const U256& q) {
 
 // (a - b) mod q for a, b < q
 __device__ __forceinline__ U256 submod256(U256 a, const U256& b, const U256& q) {
-  if (sub256(a, b)) add256(a, q);
-  return a;
+  const uint32_t borrow = sub256(a, b);
+  U256 t = a;
+  add256(t, q);
+  return sel256(0u - borrow, t, a);
 }
-// (a * b) mod q for a, b < q: left-to-right double-and-add (one thread; per proof, not per limb)
+// (a * b) mod q for a, b < q: left-to-right double-and-always-add with a masked select (one
+// thread; per proof, not per limb), so neither operand's bits steer the control flow
 __device__ __noinline__ U256 mulmod256(const U256& a, const U256& b, const U256& q) {
   U256 r;
   for (int k = 0; k < 8; ++k) r.w[k] = 0;
   for (int bit = 255; bit >= 0; --bit) {
     r = addmod256(r, r, q);
-    if ((a.w[bit >> 5] >> (bit & 31)) & 1u) r = addmod256(r, b, q);
+    const U256 t = addmod256(r, b, q);
+    r = sel256(0u - ((a.w[bit >> 5] >> (bit & 31)) & 1u), t, r);
   }
   return r;
 }

@@ -1,0 +1,85 @@
+"""GPU: the BASELINE.json configurations at one GPU's full share, checked through
+size-independent properties (the CPU oracle cannot redo them in a test's time):
+
+* configs[2] -- 8 x MI355X verify + tally of 1M ballots sharded by ballot: ONE rank's shard of
+  125,000 ballots (4 x 5 manifest), device-resident as bench.py runs it.  Every verdict is
+  valid; the tally decrypts (joint secret, BSGS dLog) to exactly the per-selection vote sums;
+  and the two-rank fold (each half verified alone, partial tallies multiplied mod p as
+  electionguard.distributed.gather_fold_tally does on rank 0) equals the single tally.
+* configs[4] -- the 100-selection manifest (20 x 5): 10,000 ballots, same checks.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(group, contests, selections, nb, seed):
+    import torch
+    from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption_device, random_scalars,
+                                      random_votes)
+    from electionguard.decrypt import dlog_g_batch
+    from electionguard.distributed import gather_fold_tally
+    from electionguard.keyceremony import key_ceremony
+    man = Manifest(contests, selections, 1)
+    gk, K = key_ceremony(group, 3, 3, seed=seed)
+    key = ElectionKey(group, K, window_bits=16)
+    rng = np.random.default_rng(seed)
+    votes = random_votes(rng, man, nb)
+    dev = torch.device("cuda", 0)
+    dv = torch.from_numpy(votes).to(dev)
+    dsn = torch.from_numpy(random_scalars(rng, (nb, man.nsel, 4), group.q)).to(dev)
+    dcn = torch.from_numpy(random_scalars(rng, (nb, man.n_contests), group.q)).to(dev)
+    cts = torch.empty((nb, man.nsel, 2, 512), dtype=torch.uint8, device=dev)
+    rp = torch.empty((nb, man.nsel, 4, 32), dtype=torch.uint8, device=dev)
+    cp = torch.empty((nb, man.n_contests, 2, 32), dtype=torch.uint8, device=dev)
+    qbar = 0xC0FFEE + seed
+    torch.cuda.synchronize()
+    batch_encryption_device(group, key, qbar, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
+                            cts.data_ptr(), rp.data_ptr(), cp.data_ptr())
+    del dsn, dcn
+    V = Verifier(group, key, qbar, man)
+
+    def verify(a, b):
+        oks = torch.zeros((b - a, man.nsel), dtype=torch.uint8, device=dev)
+        okc = torch.zeros((b - a, man.n_contests), dtype=torch.uint8, device=dev)
+        tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
+        V.verify_device(cts[a:b].data_ptr(), rp[a:b].data_ptr(), cp[a:b].data_ptr(), b - a, oks.data_ptr(),
+                        okc.data_ptr(), tal.data_ptr())
+        group.sync()
+        return bool(oks.all().item() and okc.all().item()), tal
+
+    ok, tally = verify(0, nb)
+    assert ok, "honest ballots rejected"
+    # decrypt the tally with the joint secret (quorum = all 3 guardians): t = dLog_g(beta / alpha^S)
+    S = sum(int(g.secret) for g in gk) % group.q
+    T = tally.cpu().numpy()
+    M = group.powP_batch(np.ascontiguousarray(T[:, 0]), [S] * man.n_real)
+    gt = group.multP_batch(np.ascontiguousarray(T[:, 1]), group.multInv_batch(M))
+    counts = dlog_g_batch(group, gt, nb)
+    want = votes.reshape(nb, man.n_contests, man.spc)[:, :, :man.n_selections].sum(axis=0).reshape(-1)
+    assert counts == [int(x) for x in want]
+    # two-rank shard fold == the single tally
+    h = nb // 2 + 17
+    ok_a, t_a = verify(0, h)
+    ok_b, t_b = verify(h, nb)
+    assert ok_a and ok_b
+
+    class TwoRanks:  # the gather's result for world = 2, as gather_fold_tally folds it on rank 0
+        @staticmethod
+        def is_initialized():
+            return False
+
+    parts = np.stack([t_a.cpu().numpy(), t_b.cpu().numpy()])          # (world, n_real, 2, 512)
+    g = np.ascontiguousarray(np.transpose(parts, (1, 2, 0, 3))).reshape(-1, 512)
+    folded = group.prodP_groups(g, man.n_real * 2, 2).reshape(man.n_real, 2, 512)
+    assert np.array_equal(folded, T)
+    assert gather_fold_tally(TwoRanks, tally, group.prodP_groups).tobytes() == T.tobytes()  # world 1: identity
+
+
+def test_config2_one_rank_shard_125k(group):
+    _run(group, 4, 5, 125_000, 21)
+
+
+def test_config4_shape_100_selections(group):
+    _run(group, 20, 5, 10_000, 23)
