@@ -209,13 +209,13 @@ def main():
     # HBM traffic of k_pow from the committed PMC passes of this same command
     # (tools/profile_round.sh); only quoted when the profiled workload AND the library build
     # (md5 of libeg_hip.so) match this run's.
-    prof = ROOT / "profiles" / "r01_pmc_kpow.json"
-    if prof.exists():
+    for prof in sorted((ROOT / "profiles").glob("r*_pmc_kpow.json"), reverse=True):  # newest round first
         try:
             pm = json.loads(prof.read_text())
             if pm.get("bench_config") == out["config"] and pm.get("bench_build") == build_id:
                 out["roofline"]["traffic"] = round(pm["traffic"]["hbm_bytes_per_launch"])
-                out["roofline"]["traffic_source"] = "profiles/r01_pmc_kpow.json"
+                out["roofline"]["traffic_source"] = f"profiles/{prof.name}"
+                break
         except (KeyError, ValueError, TypeError):
             pass
 

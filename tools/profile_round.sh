@@ -8,7 +8,7 @@
 #   4. --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 # then tools/prof_summary.py folds the CSVs into profiles/<tag>_*.
 set -eo pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 BENCH_ARGS=${BENCH_ARGS:-}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
