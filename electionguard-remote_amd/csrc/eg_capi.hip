@@ -140,6 +140,7 @@ struct eg_ctx {
   eg_fixed_base* gtab = nullptr;
   eg_fixed_base* Ktab = nullptr;
   uint32_t* d_gcomb = nullptr;  // Lim-Lee comb subset table of g (32 elements) for constant-time g^u
+  uint32_t hash_fmt = EG_HASH_FIXED_WIDTH;  // Fiat-Shamir pre-image hex format (eg_ctx_set_hash_format)
   DevBuf ws[W_NSLOT];
   bool timing = false;
   std::vector<ProfRec> prof;
@@ -533,6 +534,14 @@ extern "C" int eg_ctx_sync(eg_ctx* c) {
 }
 
 extern "C" eg_fixed_base* eg_ctx_g_table(eg_ctx* c) { return c ? c->gtab : nullptr; }
+
+extern "C" int eg_ctx_set_hash_format(eg_ctx* c, int format) {
+  if (!c) return fail(EG_ERR_ARG, "null ctx");
+  if (format != EG_HASH_FIXED_WIDTH && format != EG_HASH_MINIMAL) return fail(EG_ERR_ARG, "unknown hash format");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->hash_fmt = (uint32_t)format;
+  return EG_OK;
+}
 
 extern "C" int eg_fixed_base_create(eg_ctx* c, const uint8_t base_be[512], int wbits, eg_fixed_base** out) {
   if (!c || !base_be || !out) return fail(EG_ERR_ARG, "null argument");

@@ -894,7 +894,8 @@ __global__ void k_scalar_prep(const uint8_t* __restrict__ q_be, const uint8_t* _
 
 // ---------------------------------------------------------------------------------
 // Fiat-Shamir hash + compare (one thread per proof).
-//   H = SHA256("|" + hex(e_0) + "|" + ... + "|") mod q, hex upper-case fixed width.
+//   H = SHA256("|" + hex(e_0) + "|" + ... + "|") mod q, hex upper-case, fixed width or
+//   minimal-length per hash_minimal (eg_ctx_set_hash_format).
 //   selection: elements (qbar, alpha, beta, a0, b0, a1, b1), expect (c0 + c1) mod q
 //   contest  : elements (qbar, A, B, a, b),                   expect c
 // ---------------------------------------------------------------------------------
@@ -912,18 +913,19 @@ __global__ void __launch_bounds__(kBlock) k_hash_check(const uint8_t* __restrict
                                                        uint32_t proof_words, uint32_t cidx0, uint32_t cidx1,
                                                        const uint8_t* __restrict__ pre_ok,
                                                        const uint8_t* __restrict__ pre_ok2, uint32_t pre2_div,
-                                                       uint8_t* __restrict__ ok, uint8_t* __restrict__ out_h) {
+                                                       uint8_t* __restrict__ ok, uint8_t* __restrict__ out_h,
+                                                       uint32_t hash_minimal) {
   __shared__ uint32_t s_buf[kBlock * 16];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Sha256 H;
   H.init(s_buf + threadIdx.x * 16);
   H.put('|');
-  H.put_hex(qbar_be, 32);
+  H.put_hex(qbar_be, 32, hash_minimal != 0);
   H.put('|');
   const HashSrc src[6] = {s0, s1, s2, s3, s4, s5};
   for (uint32_t k = 0; k < nsrc; ++k) {
-    H.put_hex(src[k].ptr + (size_t)i * src[k].stride, src[k].bytes);
+    H.put_hex(src[k].ptr + (size_t)i * src[k].stride, src[k].bytes, hash_minimal != 0);
     H.put('|');
   }
   uint32_t dig[8];

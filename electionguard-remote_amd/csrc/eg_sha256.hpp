@@ -72,15 +72,25 @@ struct Sha256 {
   __device__ __forceinline__ static uint32_t hexc(uint32_t v) { return v < 10 ? ('0' + v) : ('A' + v - 10); }
 
   // upper-case hex of n big-endian bytes (n multiple of 16, 16-B aligned source)
-  __device__ void put_hex(const uint8_t* __restrict__ p, uint32_t n) {
+  // Upper-case hex of n big-endian bytes.  minimal = false: fixed width (2n chars);
+  // minimal = true: leading zero BYTES dropped, at least one kept (the integer's even-length
+  // hex, e.g. 0 -> "00", 0xABC -> "0ABC": electionguard-python 1.x to_hex); see
+  // eg_ctx_set_hash_format.
+  __device__ void put_hex(const uint8_t* __restrict__ p, uint32_t n, bool minimal = false) {
     const uint4* s = reinterpret_cast<const uint4*>(p);
-    for (uint32_t i = 0; i < n / 16; ++i) {
+    uint32_t first = 0;
+    if (minimal) {
+      while (first + 1 < n && p[first] == 0) ++first;
+    }
+    for (uint32_t i = first / 16; i < n / 16; ++i) {
       const uint4 v = s[i];
       const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
+          const uint32_t idx = i * 16 + k * 4 + b;
+          if (idx < first) continue;
           const uint32_t byte = (ws[k] >> (8 * b)) & 0xFF;
           put(hexc(byte >> 4));
           put(hexc(byte & 15));

@@ -208,6 +208,19 @@ class GroupContext:
     def fixed_base(self, base: Union["ElementModP", int], window_bits: int = 8) -> "FixedBase":
         return FixedBase(self, base, window_bits)
 
+    # ---- Fiat-Shamir pre-image format (unpinned upstream: switchable) ----
+    @property
+    def hash_format(self) -> str:
+        return getattr(self, "_hash_format", "fixed")
+
+    @hash_format.setter
+    def hash_format(self, fmt: str) -> None:
+        from .hashing import FORMATS
+        if fmt not in FORMATS:
+            raise ValueError(f"unknown hash format {fmt!r} (have {', '.join(FORMATS)})")
+        native.check(self._lib, "eg_ctx_set_hash_format", self._lib.eg_ctx_set_hash_format(self._ctx, FORMATS[fmt]))
+        self._hash_format = fmt
+
     # ---- profiling of the dominant kernel ----
     def profile_begin(self) -> None:
         native.check(self._lib, "eg_ctx_profile_begin", self._lib.eg_ctx_profile_begin(self._ctx))

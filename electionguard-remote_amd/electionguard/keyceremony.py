@@ -109,7 +109,8 @@ def key_ceremony(group: GroupContext, n: int, quorum: int, seed: Optional[int] =
     for i, gi in enumerate(gs):
         for j in range(quorum):
             k = i * quorum + j
-            c = hash_elems(q, ("P", gi.commitments[j]), ("P", int.from_bytes(hs[k].tobytes(), "big")))
+            c = hash_elems(q, ("P", gi.commitments[j]), ("P", int.from_bytes(hs[k].tobytes(), "big")),
+                           fmt=group.hash_format)
             gi.proofs.append((c, (us[k] - c * gi.coeffs[j]) % q))
     Ks = np.stack([np.frombuffer(p_bytes(g.public_key), dtype=np.uint8) for g in gs])
     K = int.from_bytes(group.prodP_groups(Ks, 1, n)[0].tobytes(), "big")
@@ -138,7 +139,7 @@ def verify_commitment_proofs(group: GroupContext, commitments: List[int], proofs
         c, v = proofs[k]
         K = commitments[k]
         ok = 0 < K < p and 0 <= c < q and 0 <= v < q and _be(res[k]) == 1
-        out.append(bool(ok and c == hash_elems(q, ("P", K), ("P", _be(h[k])))))
+        out.append(bool(ok and c == hash_elems(q, ("P", K), ("P", _be(h[k])), fmt=group.hash_format)))
     return out
 
 

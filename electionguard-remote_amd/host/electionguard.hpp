@@ -317,6 +317,9 @@ class GroupContext {
 
   eg_ctx* handle() const { return ctx_; }
   int device() const { return device_; }
+  // Fiat-Shamir pre-image hex form (EG_HASH_FIXED_WIDTH default / EG_HASH_MINIMAL): upstream's
+  // is unpinned, so it is switchable per context (include/eg_hip.h).
+  void setHashFormat(int format) const { check(eg_ctx_set_hash_format(ctx_, format), "eg_ctx_set_hash_format"); }
   const ElementModP& P() const { return p_; }
   const ElementModP& G() const { return g_; }
   const ElementModQ& Q() const { return q_; }

@@ -97,6 +97,10 @@ JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_gTable(JNIEnv* env, jclass 
   return (jlong)(intptr_t)eg_ctx_g_table((eg_ctx*)(intptr_t)ctx);
 }
 
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_setHashFormat(JNIEnv* env, jclass cls, jlong ctx, jint format) {
+  check_rc(env, eg_ctx_set_hash_format((eg_ctx*)(intptr_t)ctx, format));
+}
+
 /* ---------------------------------------------------------------- fixed-base tables */
 
 JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_fixedBaseCreate(JNIEnv* env, jclass cls, jlong ctx,

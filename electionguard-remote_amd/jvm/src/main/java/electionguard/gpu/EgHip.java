@@ -43,6 +43,12 @@ public final class EgHip {
   /** The fixed-base table of g built at ctxCreate (owned by the context: do not destroy). */
   public static native long gTable(long ctx);
 
+  /** Fiat-Shamir pre-image hex form: HASH_FIXED_WIDTH (default) or HASH_MINIMAL (eg_hip.h). */
+  public static final int HASH_FIXED_WIDTH = 0;
+  public static final int HASH_MINIMAL = 1;
+
+  public static native void setHashFormat(long ctx, int format);
+
   // ---- fixed-base tables (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit windows) ----
   public static native long fixedBaseCreate(long ctx, byte[] base512, int windowBits);
 

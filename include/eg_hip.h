@@ -79,6 +79,18 @@ int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_ops, double*
 /* Fixed-base table for g (built at ctx creation) — accessor. */
 eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
 
+/* Fiat-Shamir pre-image format of every hash this ctx computes (proof generation and
+ * verification): "|" + "|".join(upper-case hex of each element) + "|", SHA-256, mod q.
+ * The upstream format (electionguard-kotlin-multiplatform 1.0-SNAPSHOT hashElements) is not in
+ * the container, so both candidate hex forms are offered:
+ *   EG_HASH_FIXED_WIDTH (default): ElementModP as 1024 chars, ElementModQ as 64 (the wire widths,
+ *                                  common.proto:6-16);
+ *   EG_HASH_MINIMAL: the integer's even-length hex (leading zero bytes dropped, 0 -> "00"),
+ *                    as electionguard-python 1.x's to_hex. */
+#define EG_HASH_FIXED_WIDTH 0
+#define EG_HASH_MINIMAL 1
+int eg_ctx_set_hash_format(eg_ctx* ctx, int format);
+
 /* Fixed-base radix table (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit
  * windows).  window_bits in [4, 22]; table = ceil(256/w) * 2^w elements of 640 B
  * in HBM (w = 16: 671 MB, w = 22: 32 GB). */

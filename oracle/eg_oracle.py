@@ -148,12 +148,38 @@ class Group:
 # ElementModQ -> 64 hex chars (32 B BE, common.proto:12-16).  Unpinned upstream.
 # --------------------------------------------------------------------------------------
 
+# The hex form is switchable because upstream's is unpinned: "fixed" (the default above) or
+# "minimal" (the integer's even-length hex, leading zero bytes dropped, 0 -> "00": the
+# electionguard-python 1.x to_hex form).  Tests switch it with `with hash_format("minimal"):`.
+HASH_FORMAT = "fixed"
+
+
+class hash_format:
+    def __init__(self, fmt: str):
+        assert fmt in ("fixed", "minimal")
+        self.fmt = fmt
+
+    def __enter__(self):
+        global HASH_FORMAT
+        self.prev, HASH_FORMAT = HASH_FORMAT, self.fmt
+
+    def __exit__(self, *exc):
+        global HASH_FORMAT
+        HASH_FORMAT = self.prev
+
+
+def _hexb(b: bytes) -> str:
+    if HASH_FORMAT == "minimal":
+        b = b.lstrip(b"\0") or b"\0"
+    return b.hex().upper()
+
+
 def hexP(x: int) -> str:
-    return x.to_bytes(512, "big").hex().upper()
+    return _hexb(x.to_bytes(512, "big"))
 
 
 def hexQ(x: int) -> str:
-    return x.to_bytes(32, "big").hex().upper()
+    return _hexb(x.to_bytes(32, "big"))
 
 
 def hash_elems(q: int, *elems: Tuple[str, int]) -> int:

@@ -130,12 +130,18 @@ def test_python_oracle_trustee_golden(mode):
         assert O.verify_share(G, qbar, gs[0].K, texts[i], M, pr)
 
 
-def test_hash_host_matches_oracle():
-    from electionguard.core.hashing import hash_elems
+@pytest.mark.parametrize("fmt", ["fixed", "minimal"])
+def test_hash_host_matches_oracle(fmt):
+    from electionguard.core.hashing import hash_elems, hexP, hexQ
     rng = random.Random(9)
     for _ in range(5):
-        els = [("Q", rng.randrange(2**256))] + [("P", rng.randrange(2**4096)) for _ in range(3)]
-        assert hash_elems(O.Q, *els) == O.hash_elems(O.Q, *els)
+        els = [("Q", rng.randrange(2**256))] + [("P", rng.randrange(2**4096)) for _ in range(3)] + \
+              [("P", rng.randrange(2**100)), ("Q", 0), ("P", 5)]
+        with O.hash_format(fmt):
+            assert hash_elems(O.Q, *els, fmt=fmt) == O.hash_elems(O.Q, *els)
+    # the minimal form is electionguard-python's to_hex: even length, leading zero bytes dropped
+    assert (hexQ(0, "minimal"), hexQ(5, "minimal"), hexP(0xABC, "minimal")) == ("00", "05", "0ABC")
+    assert len(hexP(5, "fixed")) == 1024 and len(hexQ(5, "fixed")) == 64
 
 
 # --------------------------------------------------------------------------------------
