@@ -21,6 +21,10 @@ constexpr int kBlock = 256;
 #ifndef EG_MIN_WAVES
 #define EG_MIN_WAVES 3  // k_pow: 3 waves/SIMD (<= 168 VGPRs; a few squaring-loop spills, measured +1.3..1.6%)
 #endif
+#ifndef EG_PREFETCH
+#define EG_PREFETCH 0  // k_pow: 1 = prefetch the next radix-table entry of a fixed-base run, 2 = also the
+                       // next comb-table entry.  Off: measured no gain
+#endif
 constexpr int kGroupsPerBlock = kBlock / kT;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -83,6 +87,17 @@ __device__ __forceinline__ uint32_t* group_slot() {
 __device__ __forceinline__ uint32_t group_id() { return blockIdx.x * kGroupsPerBlock + threadIdx.x / kT; }
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// Pull the five 128-B lines of a device element toward the CU while the current multiply
+// runs, without holding a VGPR across it: one LDS-DMA dword per lane (group lane l reads word
+// 20 l, which touches every line of the 640-B element) into a per-wave discard buffer that
+// nothing reads.  The later elem_to_lds of the same element then hits in L2.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+__device__ __forceinline__ void prefetch_elem(const uint32_t* e, uint32_t* wave_discard) {
+  __builtin_amdgcn_global_load_lds((glb_void_t*)const_cast<uint32_t*>(e + glane() * kLP),
+                                   (lds_void_t*)wave_discard, 4, 0, 0);
+}
 
 // x <- x * x
 template <bool F>
@@ -340,23 +355,6 @@ __device__ __forceinline__ uint32_t be_digit(const uint8_t* __restrict__ e, int 
   return (v >> (bit & 7)) & ((1u << wb) - 1u);
 }
 
-template <bool F>
-__device__ __forceinline__ void fb_ladder(const Mont<F>& M, uint32_t (&x)[kL], uint32_t* slot, const FbTab& T,
-                                          const uint8_t* __restrict__ e, bool x_is_one) {
-  const uint32_t wb = T.wbits;
-  uint32_t k0 = 0;
-  if (x_is_one) {
-    const uint32_t d = be_digit(e, 32, 0, wb);
-    load_elem(x, T.data + (size_t)d * kW);
-    k0 = 1;
-  }
-#pragma unroll 1
-  for (uint32_t k = k0; k < T.nwin; ++k) {
-    const uint32_t d = be_digit(e, 32, k * wb, wb);
-    mmul_g(M, x, slot, T.data + ((size_t)(k << wb) + d) * kW);
-  }
-}
-
 // One launch may carry two job populations of different shapes (e.g. the beta jobs and the
 // contest-A jobs that only depend on the previous launch): part 0 owns the first P0.nblocks
 // workgroups, part 1 the rest, so the short part-1 jobs fill the tail of part 0 instead of
@@ -383,6 +381,10 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
                                                 const uint8_t* __restrict__ scalars,
                                                 uint32_t* __restrict__ out, FbTab fb0, FbTab fb1) {
   __shared__ uint8_t s_dig[kGroupsPerBlock][64];
+#if EG_PREFETCH
+  __shared__ uint32_t s_pf[kBlock / kWave][kWave];  // prefetch_elem discard buffers
+  uint32_t* const pf_discard = s_pf[threadIdx.x / kWave];
+#endif
   const bool second = blockIdx.x >= P0.nblocks;
   const PowPart& P = second ? P1 : P0;  // kernarg memory: shape fields stay scalar loads
   const PowShape& S = P.S;
@@ -443,6 +445,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   }
   while (true) {
     const uint32_t* ysrc = nullptr;  // nullptr: square
+    const uint32_t* pf = nullptr;    // table entry of a later multiply, fetched during this one
     bool done = false;
     while (true) {
       if (phase == kPre) {  // k squarings done so far
@@ -541,6 +544,9 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         if (w < 0) { t = 0; kf = 0; phase = kFb; continue; }
         if (sub == 0) break;  // square
         ysrc = tbl + (size_t)dig[w] * kW;
+#if EG_PREFETCH >= 2
+        if (!CT && w > 0) pf = tbl + (size_t)dig[w - 1] * kW;  // after the next squaring
+#endif
         break;
       }
       if (phase == kVar) {
@@ -565,6 +571,12 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       const uint32_t* ent = T.data + ((size_t)(kf << T.wbits) + d) * kW;
       if (x_is_one) { load_elem(x, ent); x_is_one = false; ++kf; continue; }
       ysrc = ent;
+#if EG_PREFETCH
+      if (kf + 1 < T.nwin) {
+        const uint32_t d1 = be_digit(scalars + (size_t)J[5 + 2 * o + t] * 32, 32, (kf + 1) * T.wbits, T.wbits);
+        pf = T.data + ((size_t)((kf + 1) << T.wbits) + d1) * kW;
+      }
+#endif
       break;
     }
     if (done) break;
@@ -577,6 +589,9 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         elem_to_lds(slot, ysrc);
       }
       wave_sync();
+#if EG_PREFETCH
+      if (pf) prefetch_elem(pf, pf_discard);
+#endif
       M.mul(x, slot);
     } else {
       regs_to_lds(slot, x);
@@ -601,6 +616,10 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     else if (phase == kComb) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
     else { ++kf; }
   }
+#if EG_PREFETCH
+  // no LDS-DMA write may land after the workgroup's LDS is handed to another workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 
 // ---------------------------------------------------------------------------------
