@@ -565,8 +565,12 @@ static int upload(eg_ctx* c, Slot s, const void* h, size_t bytes, void** d) {
   return EG_OK;
 }
 
+// Element and job indices are 32-bit on the device: one call takes at most 2^31 elements.
+constexpr size_t kMaxBatch = (size_t)1 << 31;
+
 static int pow_host(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint32_t exp_bytes, bool exp_shared,
                     uint8_t* out_be, size_t n, const FbTab* fbonly) {
+  if (n > kMaxBatch) return fail(EG_ERR_ARG, "batch too large");
   uint8_t *d_base = nullptr, *d_exp = nullptr, *d_out = nullptr;
   uint32_t *d_e = nullptr, *d_o = nullptr, *d_jobs = nullptr;
   int rc;
@@ -641,6 +645,7 @@ extern "C" int eg_multinv_batch(eg_ctx* c, const uint8_t* a_be, uint8_t* out_be,
 extern "C" int eg_multp_batch(eg_ctx* c, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be, size_t n) {
   if (!c || (n && (!a_be || !b_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
   if (!n) return EG_OK;
+  if (n > kMaxBatch) return fail(EG_ERR_ARG, "batch too large");
   Locked L(c);
   uint8_t *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
   uint32_t *ea = nullptr, *eb = nullptr;
@@ -670,6 +675,7 @@ extern "C" int eg_prod_reduce(eg_ctx* c, const uint8_t* elems_be, size_t groups,
     for (size_t g = 0; g < groups; ++g) out_be[g * 512 + 511] = 1;
     return EG_OK;
   }
+  if (groups > kMaxBatch || len > kMaxBatch || groups * len > kMaxBatch) return fail(EG_ERR_ARG, "batch too large");
   const size_t n = groups * len;
   uint8_t *d_in = nullptr, *d_out = nullptr;
   uint32_t *e = nullptr, *o = nullptr;
@@ -754,7 +760,7 @@ static int identity_pow_jobs(eg_ctx* c, size_t n, bool fbonly, const uint32_t** 
 
 static int pow_dev(eg_ctx* c, const uint8_t* d_base_be, const uint8_t* d_exp_be, uint8_t* d_out_be, size_t n,
                    const FbTab* fbonly) {
-  if (n > ((size_t)1 << 31)) return fail(EG_ERR_ARG, "batch too large");
+  if (n > kMaxBatch) return fail(EG_ERR_ARG, "batch too large");
   const uint32_t* d_jobs = nullptr;
   uint32_t *d_e = nullptr, *d_o = nullptr;
   int rc;

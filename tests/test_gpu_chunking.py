@@ -186,3 +186,65 @@ def test_host_pointer_encryption_equals_device_resident_with_wide_contests(group
     assert np.array_equal(oc.cpu().numpy(), eb.cts)
     assert np.array_equal(orp.cpu().numpy(), eb.rproof)
     assert np.array_equal(ocp.cpu().numpy(), eb.cproof)
+
+
+def test_wide_manifest_smaller_chunks(group):
+    """A 200-selection contest (201 jobs per ballot) lowers the chunk to 2^21 // 201 = 10,433
+    ballots (eg_capi_ballot.inc ballot_chunk), so 10,463 ballots run as two verify chunks and
+    two encryption chunks: a ballot's bytes must not depend on its chunk, every proof
+    verifies, the running tally equals the product of the two halves' tallies (and CPython's
+    product for a few selections), and a tamper in the second chunk is flagged exactly."""
+    from electionguard.ballot import (ElectionKey, EncryptedBallots, Manifest, Verifier, batch_encryption,
+                                      random_scalars, random_votes)
+    from electionguard.keyceremony import key_ceremony
+    man = Manifest(1, 200, 1)
+    chunk = (1 << 21) // man.nsel
+    assert chunk == 10433
+    nb = chunk + 30
+    _, K = key_ceremony(group, 2, 2, seed=83)
+    key = ElectionKey(group, K, window_bits=12)
+    rng = np.random.default_rng(83)
+    votes = random_votes(rng, man, nb)
+    sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
+    cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    eb = batch_encryption(group, key, 4242, man, votes, sn, cn)
+    a, b = chunk - 4, chunk + 4
+    part = batch_encryption(group, key, 4242, man, votes[a:b], sn[a:b], cn[a:b])
+    assert np.array_equal(part.cts, eb.cts[a:b]) and np.array_equal(part.rproof, eb.rproof[a:b])
+    assert np.array_equal(part.cproof, eb.cproof[a:b])
+    V = Verifier(group, key, 4242, man)
+    ok_s, ok_c, tally = V.verify(eb)
+    assert ok_s.all() and ok_c.all()
+    _, _, t1 = V.verify(eb.slice(0, chunk))
+    _, _, t2 = V.verify(eb.slice(chunk, nb))
+    prod = group.multP_batch(t1.reshape(-1, 512), t2.reshape(-1, 512)).reshape(tally.shape)
+    assert np.array_equal(prod, tally)
+    p = O.production_group().p
+    for s in (0, 117, 199):
+        for comp in range(2):
+            acc = 1
+            for row in eb.cts[:, s, comp]:
+                acc = acc * int.from_bytes(row.tobytes(), "big") % p
+            assert int.from_bytes(tally[s, comp].tobytes(), "big") == acc, (s, comp)
+    rp = eb.rproof.copy()
+    rp[chunk + 11, 150, 0, 7] ^= 0x10
+    ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, eb.cproof), with_tally=False)
+    assert np.argwhere(~ok_s).tolist() == [[chunk + 11, 150]] and ok_c.all()
+
+
+def test_oversized_arguments_rejected(group):
+    """Batches past the 32-bit device index range and manifests wider than 2^20 selections
+    per ballot fail with EG_ERR_ARG before anything is read or allocated."""
+    import ctypes
+    lib = group._lib
+    one = ctypes.create_string_buffer(512)
+    rc = lib.eg_powp_batch(group.handle, one, one, one, (1 << 31) + 1)
+    assert rc == 1 and b"batch too large" in lib.eg_last_error()
+    rc = lib.eg_multp_batch(group.handle, one, one, one, (1 << 31) + 1)
+    assert rc == 1
+    rc = lib.eg_prod_reduce(group.handle, one, 1 << 16, 1 << 16, one)
+    assert rc == 1
+    rc = lib.eg_verify_ballots_dev(group.handle, one, 1, 1 << 21, 1, 0, 1, one, one, one, one, one, None)
+    assert rc == 1 and b"manifest" in lib.eg_last_error()
+    rc = lib.eg_encrypt_ballots(group.handle, one, 1, 1 << 11, 1 << 10, one, one, one, one, one, one)
+    assert rc == 1 and b"manifest" in lib.eg_last_error()
