@@ -116,6 +116,16 @@ struct ProfRec {
   double sqr;  // of which squarings (symmetric-half schedule)
 };
 
+// Montgomery operations of one k_pow job, split into squarings and multiplies: counted from
+// the job's op program itself (pow_schedule), so the profile's MM totals are the kernel's work.
+struct MMCount {
+  double mul = 0, sqr = 0;
+};
+struct SchedBuf {
+  const uint32_t* ptr;
+  MMCount mm;
+};
+
 struct eg_fixed_base {
   eg_ctx* ctx = nullptr;
   uint32_t* d_tab = nullptr;
@@ -146,6 +156,7 @@ struct eg_ctx {
   std::vector<ProfRec> prof;
   uint8_t K_be[512];
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
+  std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
   // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
   // most recently used first
@@ -197,51 +208,129 @@ static int launch_export(eg_ctx* c, const uint32_t* d_in, size_t n, uint8_t* d_b
   return EG_OK;
 }
 
-// Montgomery operations of one k_pow job, split into squarings and multiplies
-// (mirrors the kernel's state machine: kPre / kComb-even / kVar sub<4 steps square).
-struct MMCount {
-  double mul = 0, sqr = 0;
-};
-static MMCount pow_job_mm(const MontConsts& H, const PowShape& S, const FbTab& f0, const FbTab& f1) {
+// Compile a launch shape into k_pow's op program (eg_kernels.hpp, PowOp).  The order of the
+// multiplies is the algorithm:
+//   window     : table B^0..B^15 (14 MM); per exponent MSB-first 4-bit windows, 4 sq + 1 mul
+//   comb       : y_k = B^(2^(52k)) (208 sq, kept in yout for gather jobs), the 32 subset
+//                products (26 MM), per exponent 51 x (1 sq + 1 mul) from column digits
+//   gather     : y_k = prod of the factor jobs' y_k (4 x (gather-1) MM instead of 208 sq)
+//   resid      : 48 more squarings past y_4 give z = B^(2^256); w = B^c by a left-to-right
+//                ladder over the public c = 2^256 - q; both to rout (k_resid_check: z == w)
+//   fixed base : radix-table windows of g / K per term; the first one loads instead of multiplying
+static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S, const FbTab& f0, const FbTab& f1,
+                                          MMCount* mm) {
+  std::vector<uint32_t> v;
   MMCount n;
-  if (S.has_base && !(S.comb && S.shared_comb)) {
-    if (S.comb) {
-      if (S.gather)
-        n.mul += (double)((kCombH - 1) * (S.gather - 1));  // y_k gathered from the factors' y_k
-      else
-        n.sqr += (double)((kCombH - 1) * kCombW);
-      n.mul += (double)((1 << kCombH) - kCombH - 1);
-      if (S.resid && !S.gather && H.qc_bits) {  // z: 48 squarings past y_4; w = B^c ladder
-        int pop = 0;
-        for (int w = 0; w < 8; ++w) pop += __builtin_popcount(H.qc[w]);
-        n.sqr += (double)(256 - (kCombH - 1) * kCombW) + (double)(H.qc_bits - 1);
-        n.mul += (double)(pop - 1);
+  auto op = [&](PowOp k, uint32_t arg = 0) {
+    v.push_back(pow_op(k, arg));
+    if (k == OP_SQR) n.sqr += 1;
+    else if (k != OP_END && k <= kOpMulLast) n.mul += 1;
+  };
+  const bool comb = S.comb != 0;
+  if (S.has_base && !(comb && S.shared_comb)) {
+    op(OP_LOAD_ONE);
+    op(OP_STORE_TBL, 0);
+    op(OP_LOAD_BASE);
+    op(OP_STORE_TBL, 1);
+    if (!comb) {
+      for (uint32_t k = 2; k < 16; ++k) {
+        op(OP_MUL_BASE);
+        op(OP_STORE_TBL, k);
       }
     } else {
-      n.mul += 14.0;
+      if (S.gather) {
+        for (uint32_t k = 1; k < (uint32_t)kCombH; ++k) {
+          op(OP_LOAD_GATHER, k - 1);
+          for (uint32_t i = 1; i < S.gather; ++i) op(OP_MUL_GATHER, i << 2 | (k - 1));
+          op(OP_STORE_TBL, 1u << k);
+        }
+      } else {
+        for (uint32_t k = 1; k <= (uint32_t)((kCombH - 1) * kCombW); ++k) {
+          op(OP_SQR);
+          if (k % kCombW == 0) {
+            op(OP_STORE_TBL, 1u << (k / kCombW));
+            op(OP_STORE_Y, k / kCombW - 1);
+          }
+        }
+        if (S.resid) {
+          for (uint32_t k = (kCombH - 1) * kCombW; k < 256; ++k) op(OP_SQR);
+          op(OP_STORE_R, 0);
+          op(OP_LOAD_TBL, 1);
+          for (int w = (int)H.qc_bits - 2; w >= 0; --w) {
+            op(OP_SQR);
+            if ((H.qc[w >> 5] >> (w & 31)) & 1u) op(OP_MUL_TBL, 1);
+          }
+          op(OP_STORE_R, 1);
+        }
+      }
+      for (uint32_t k = 3; k < (1u << kCombH); ++k) {
+        if ((k & (k - 1)) == 0) continue;
+        op(OP_LOAD_TBL, k & (k - 1));
+        op(OP_MUL_TBL, k & (0u - k));
+        op(OP_STORE_TBL, k);
+      }
     }
   }
   for (uint32_t o = 0; o < S.nout; ++o) {
     bool one = true;
     if (S.has_base) {
-      const double steps = S.comb ? (double)(kCombW - 1) : (double)(S.exp_bytes * 2 - 1);
-      n.sqr += steps * (S.comb ? 1.0 : 4.0);
-      n.mul += steps;
+      op(OP_EXP, o);
+      if (comb) {
+        op(OP_LOAD_COMB, kCombW - 1);
+        for (int w = kCombW - 2; w >= 0; --w) {
+          op(OP_SQR);
+          op(OP_MUL_COMB, (uint32_t)w);
+        }
+      } else {
+        op(OP_LOAD_WIN, o);
+        for (uint32_t w = 1; w < S.exp_bytes * 2; ++w) {
+          for (int i = 0; i < 4; ++i) op(OP_SQR);
+          op(OP_MUL_WIN, w | o << 12);
+        }
+      }
       one = false;
     }
     for (uint32_t t = 0; t < S.nfb[o]; ++t) {
-      const FbTab& T = S.tab[o][t] ? f1 : f0;
-      n.mul += (double)T.nwin - (one ? 1.0 : 0.0);
-      one = false;
+      const uint32_t tab = S.tab[o][t] ? 1u : 0u;
+      const FbTab& T = tab ? f1 : f0;
+      for (uint32_t kf = 0; kf < T.nwin; ++kf) {
+        op(one ? OP_LOAD_FB : OP_MUL_FB, fb_arg(o, t, tab, kf));
+        one = false;
+      }
     }
+    if (one) op(OP_LOAD_ONE);
+    op(OP_STORE_OUT, o);
   }
+  op(OP_END);
 #if !EG_SQR
   n.mul += n.sqr;  // squarings run the plain multiply schedule
   n.sqr = 0;
 #endif
-  return n;
+  if (mm) *mm = n;
+  return v;
 }
 
+// The device copy of a shape's op program, compiled once per (shape, tables) and kept for
+// the context's lifetime (a few dozen distinct shapes at most).
+static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const FbTab& f1, const uint32_t** d_sched,
+                            MMCount* mm) {
+  std::string key((const char*)&S, sizeof(S));
+  key.append((const char*)&f0.nwin, 4).append((const char*)&f1.nwin, 4);
+  auto it = c->sched.find(key);
+  if (it == c->sched.end()) {
+    MMCount n;
+    // fb_arg holds the window index in 8 bits: window_bits >= 4 gives at most 64 windows
+    if (f0.nwin > 256 || f1.nwin > 256) return fail(EG_ERR_ARG, "fixed-base table has too many windows");
+    std::vector<uint32_t> prog = pow_schedule(c->h, S, f0, f1, &n);
+    void* d = nullptr;
+    HIPCHK(hipMalloc(&d, prog.size() * 4));
+    HIPCHK(hipMemcpy(d, prog.data(), prog.size() * 4, hipMemcpyHostToDevice));
+    it = c->sched.emplace(key, SchedBuf{(const uint32_t*)d, n}).first;
+  }
+  *d_sched = it->second.ptr;
+  if (mm) *mm = it->second.mm;
+  return EG_OK;
+}
 
 // Run a homogeneous batch of exponentiation jobs (device job records).
 // yout (comb jobs, optional): y_1..y_4 of every job, (kCombH-1) device elements per job, kept for a
@@ -277,8 +366,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   const size_t per1 = tail ? pow_scratch_per_group(tail->S) : 0;
   // bound the per-launch scratch (table of 16/32 powers per job)
   const size_t max_jobs = (size_t)1 << 18;
-  const MMCount mm_job = pow_job_mm(c->h, S, f0, f1);
-  const MMCount mm_tail = tail ? pow_job_mm(c->h, tail->S, f0, f1) : MMCount{};
+  MMCount mm_job, mm_tail;
+  const uint32_t *sched = nullptr, *sched_tail = nullptr;
+  int src = pow_schedule_dev(c, S, f0, f1, &sched, &mm_job);
+  if (!src && tail) src = pow_schedule_dev(c, tail->S, f0, f1, &sched_tail, &mm_tail);
+  if (src) return src;
   size_t off = 0;
   do {
     const size_t nj = std::min(max_jobs, njobs - off);
@@ -287,11 +379,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     uint32_t* scr = nullptr;
     int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
     if (rc) return rc;
-    PowPart P0{S, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
+    PowPart P0{S, sched, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
                yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat, rout ? rout + off * 2 * kW : nullptr, ctab};
     PowPart P1{};
     if (nt) {
-      P1 = PowPart{tail->S, tail->jobs, (uint32_t)nt, grid_for(nt),
+      P1 = PowPart{tail->S, sched_tail, tail->jobs, (uint32_t)nt, grid_for(nt),
                    scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, nullptr, nullptr};
     }
     ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
@@ -509,6 +601,7 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
     if (b.ptr) hipFree(b.ptr);
   for (auto& kv : c->cache)
     if (kv.second.ptr) hipFree(kv.second.ptr);
+  for (auto& kv : c->sched) hipFree(const_cast<uint32_t*>(kv.second.ptr));
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);

@@ -21,10 +21,6 @@ constexpr int kBlock = 256;
 #ifndef EG_MIN_WAVES
 #define EG_MIN_WAVES 3  // k_pow: 3 waves/SIMD (<= 168 VGPRs; a few squaring-loop spills, measured +1.3..1.6%)
 #endif
-#ifndef EG_PREFETCH
-#define EG_PREFETCH 0  // k_pow: 1 = prefetch the next radix-table entry of a fixed-base run, 2 = also the
-                       // next comb-table entry.  Off: measured no gain
-#endif
 constexpr int kGroupsPerBlock = kBlock / kT;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -88,15 +84,18 @@ __device__ __forceinline__ uint32_t group_id() { return blockIdx.x * kGroupsPerB
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
-// Pull the five 128-B lines of a device element toward the CU while the current multiply
-// runs, without holding a VGPR across it: one LDS-DMA dword per lane (group lane l reads word
-// 20 l, which touches every line of the 640-B element) into a per-wave discard buffer that
-// nothing reads.  The later elem_to_lds of the same element then hits in L2.
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
-__device__ __forceinline__ void prefetch_elem(const uint32_t* e, uint32_t* wave_discard) {
-  __builtin_amdgcn_global_load_lds((glb_void_t*)const_cast<uint32_t*>(e + glane() * kLP),
-                                   (lds_void_t*)wave_discard, 4, 0, 0);
+// A copy of a loop-invariant pointer that the compiler cannot see through: loads from it stay
+// where they are written instead of being hoisted out of k_pow's op loop and held in VGPRs
+// across every multiply (v: per-lane pointer, s: wave-uniform pointer).
+template <class T>
+__device__ __forceinline__ T* opaque_v(T* q) {
+  asm volatile("" : "+v"(q));
+  return q;
+}
+template <class T>
+__device__ __forceinline__ T* opaque_s(T* q) {
+  asm volatile("" : "+s"(q));
+  return q;
 }
 
 // x <- x * x
@@ -355,12 +354,51 @@ __device__ __forceinline__ uint32_t be_digit(const uint8_t* __restrict__ e, int 
   return (v >> (bit & 7)) & ((1u << wb) - 1u);
 }
 
+// A k_pow job is a straight-line program over one register element x (its group's 8 lanes):
+// the host compiles every launch shape into a list of op words (pow_schedule in eg_capi.hip),
+// the same list for every job of the launch, and k_pow interprets it.  The op word is read
+// with a scalar load and every branch is wave-uniform; only the operands differ per job
+// (the base J[0], exponents J[1..2], fixed-base scalars J[5..8] and outputs J[3..4]).
+// Keeping the control state to one program counter (instead of a phase state machine)
+// leaves the multiply bodies with fewer live registers and no per-multiply bookkeeping.
+//   op = kind | arg << kOpShift
+enum PowOp : uint32_t {
+  OP_END = 0,
+  OP_SQR,         // x <- x^2
+  OP_MUL_BASE,    // x <- x * B
+  OP_MUL_TBL,     // x <- x * tbl[arg]
+  OP_MUL_WIN,     // x <- x * tbl[nibble w of exponent J[1 + o]], arg = w | o << 12 (4-bit window, MSB first)
+  OP_MUL_COMB,    // x <- x * tbl[dig[arg]]                      (Lim-Lee column arg)
+  OP_MUL_GATHER,  // x <- x * y_{k}(job J[2] + i), arg = i << 2 | (k - 1)
+  OP_MUL_FB,      // x <- x * T[kf][digit kf of scalar J[5 + 2o + t]], arg = fb_arg(o, t, tab, kf)
+  OP_LOAD_ONE,    // x <- R mod p
+  OP_LOAD_BASE,   // x <- B
+  OP_LOAD_TBL,    // x <- tbl[arg]
+  OP_LOAD_WIN,    // x <- tbl[nibble 0 of exponent J[1 + arg]]
+  OP_LOAD_COMB,   // x <- tbl[dig[arg]]
+  OP_LOAD_GATHER, // x <- y_{arg + 1}(job J[2])
+  OP_LOAD_FB,     // x <- T[kf][digit], arg as OP_MUL_FB
+  OP_STORE_TBL,   // tbl[arg] <- x
+  OP_STORE_Y,     // yout[job][arg] <- x                         (if the part has yout)
+  OP_STORE_R,     // rout[job][arg] <- x                         (residue pair)
+  OP_STORE_OUT,   // out[J[3 + arg]] <- x
+  OP_EXP,         // comb shapes: spread the column digits of exponent J[1 + arg] to dig[]
+};
+constexpr uint32_t kOpShift = 5;
+constexpr uint32_t kOpMulLast = OP_MUL_FB;
+__host__ __device__ constexpr uint32_t pow_op(PowOp k, uint32_t arg = 0) { return (uint32_t)k | (arg << kOpShift); }
+// fixed-base operand: window kf (< 256) of term t (< 2) of output o (< 2) from table tab (0 = fb0)
+__host__ __device__ constexpr uint32_t fb_arg(uint32_t o, uint32_t t, uint32_t tab, uint32_t kf) {
+  return kf | (t << 8) | (o << 9) | (tab << 10);
+}
+
 // One launch may carry two job populations of different shapes (e.g. the beta jobs and the
 // contest-A jobs that only depend on the previous launch): part 0 owns the first P0.nblocks
 // workgroups, part 1 the rest, so the short part-1 jobs fill the tail of part 0 instead of
 // running as a separate, under-filled launch.  The shape stays workgroup-uniform.
 struct PowPart {
   PowShape S;
+  const uint32_t* sched;  // the shape's op program (pow_schedule), OP_END-terminated
   const uint32_t* jobs;
   uint32_t njobs;
   uint32_t nblocks;   // workgroups of this part
@@ -381,132 +419,95 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
                                                 const uint8_t* __restrict__ scalars,
                                                 uint32_t* __restrict__ out, FbTab fb0, FbTab fb1) {
   __shared__ uint8_t s_dig[kGroupsPerBlock][64];
-#if EG_PREFETCH
-  __shared__ uint32_t s_pf[kBlock / kWave][kWave];  // prefetch_elem discard buffers
-  uint32_t* const pf_discard = s_pf[threadIdx.x / kWave];
-#endif
   const bool second = blockIdx.x >= P0.nblocks;
   const PowPart& P = second ? P1 : P0;  // kernarg memory: shape fields stay scalar loads
   const PowShape& S = P.S;
-  const uint32_t* __restrict__ jobs = P.jobs;
+  // the op program is read-only for the kernel's lifetime: through the constant address space
+  // its words are scalar loads (s_load), not vector loads plus readfirstlane
+  typedef __attribute__((address_space(4))) const uint32_t const_u32;
+  const const_u32* sched = (const const_u32*)P.sched;
   const uint32_t njobs = P.njobs;
-  uint32_t* __restrict__ scratch = P.scratch;
-  uint32_t* __restrict__ yout = P.yout;
-  const uint32_t* __restrict__ ygat = P.ygat;
-  const uint32_t gid = (blockIdx.x - (second ? P0.nblocks : 0u)) * kGroupsPerBlock + threadIdx.x / kT;
-  const uint32_t jb = gid < njobs ? gid : njobs - 1;
-  const uint32_t* J = jobs + (size_t)jb * kJobWords;
+  const uint32_t gid0 = (blockIdx.x - (second ? P0.nblocks : 0u)) * kGroupsPerBlock;  // wave-uniform
   uint32_t* slot = group_slot();
   uint8_t* dig = s_dig[threadIdx.x / kT];
   Mont<F> M;
   M.load(C);
   uint32_t x[kL];
-  const bool comb = S.comb != 0;
-  const uint32_t tsize = comb ? (1u << kCombH) : 16u;
-  // shared comb table (read-only: its precompute phases are skipped) or the job's scratch table
-  uint32_t* tbl = (comb && S.shared_comb) ? const_cast<uint32_t*>(P.ctab) : scratch + (size_t)gid * tsize * kW;
+  const uint32_t tsize = S.comb ? (1u << kCombH) : 16u;
+  const uint32_t gid = gid0 + threadIdx.x / kT;
+  const bool live = gid < njobs;  // tail groups recompute job njobs-1 and store nothing
+  const uint32_t* J = P.jobs + (size_t)(live ? gid : njobs - 1) * kJobWords;
+  // shared comb table (read-only: the schedule has no precompute) or the job's scratch table
+  uint32_t* tbl = (S.comb && S.shared_comb) ? const_cast<uint32_t*>(P.ctab) : P.scratch + (size_t)gid * tsize * kW;
   const uint32_t* B = (S.has_base && !S.shared_comb) ? elems + (size_t)J[0] * kW : nullptr;
-  const int nwin = (int)S.exp_bytes * 2;
 
-  // The whole job is one stream of Montgomery multiplies x <- x * Y driven by a small
-  // state machine, so the multiply body is inlined exactly once (register allocation
-  // of one ~150-VGPR body instead of several).  All branches are launch-uniform.
-  //   window path: table B^0..B^15 (14 MM), per exponent 63 x (4 sq + 1 mul)
-  //   comb path  : y_k = B^(2^(52k)) (208 sq), table of the 32 subset products (26 MM),
-  //                per exponent 51 x (1 sq + 1 mul) from column digits; yout (if set) keeps
-  //                y_1..y_4 of every job for a later gather launch
-  //   gather     : B = prod of S.gather comb bases whose y_k are in ygat (jobs J[2] ..):
-  //                y_k = prod of theirs, 4 x (gather-1) MM instead of 208 squarings
-  //   resid      : after y_4, 48 more squarings give z = B^(2^256); then w = B^c by a public
-  //                left-to-right binary ladder over c = 2^256 - q (C->qc); both to rout
-  uint32_t* __restrict__ rout = P.rout;
-  enum : int { kTable = 0, kVar = 1, kFb = 2, kBegin = 3, kPre = 4, kCTab = 5, kComb = 6, kGather = 7,
-               kRsq = 8, kRc = 9 };
-  int phase = kBegin, k = 2, w = 0, sub = 0;
-  uint32_t o = 0, t = 0, kf = 0;
-  bool x_is_one = true;
-  const uint8_t* e = nullptr;
-  if (S.has_base && comb && S.shared_comb) {
-    phase = kBegin;  // the table is ready
-  } else if (S.has_base) {
-    uint32_t one[kL];
-    load_elem(one, C->one);
-    store_elem(tbl, one);
-    load_elem(x, B);
-    store_elem(tbl + kW, x);
-    phase = comb ? kPre : kTable;
-    k = comb ? 0 : 2;
-    if (comb && S.gather) {
-      phase = kGather;
-      k = 1;
-      sub = 1;
-      load_elem(x, ygat + ((size_t)J[2] * (kCombH - 1)) * kW);
-    }
-  }
+  // Outer loop: one Montgomery multiply (or square) per trip, at a single inlined site; the
+  // inner loop runs the program's loads, stores and digit spreads up to the next multiply.
+  uint32_t pc = 0;
+#ifdef EG_XINIT
+  load_elem(x, C->one);
+#endif
   while (true) {
     const uint32_t* ysrc = nullptr;  // nullptr: square
-    const uint32_t* pf = nullptr;    // table entry of a later multiply, fetched during this one
-    bool done = false;
+    uint32_t kind = OP_END, arg = 0;
     while (true) {
-      if (phase == kPre) {  // k squarings done so far
-        if (k < (kCombH - 1) * kCombW) break;  // square
-        if (S.resid) { phase = kRsq; continue; }
-        phase = kCTab;
-        k = 3;
-        continue;
-      }
-      if (phase == kRsq) {  // z = B^(2^256): squarings 208..255 continue from y_4
-        if (k < 256) break;  // square
-        if (gid < njobs) store_elem(rout + (size_t)gid * 2 * kW, x);
-        load_elem(x, tbl + kW);  // B
-        w = (int)C->qc_bits - 2;
-        sub = 0;
-        phase = kRc;
-        continue;
-      }
-      if (phase == kRc) {  // w = B^c, bits qc_bits-2 .. 0 of the public c
-        if (w < 0) {
-          if (gid < njobs) store_elem(rout + ((size_t)gid * 2 + 1) * kW, x);
-          phase = kCTab;
-          k = 3;
-          continue;
-        }
-        if (sub == 0) break;  // square
-        if ((C->qc[w >> 5] >> (w & 31)) & 1u) { ysrc = tbl + kW; break; }
-        sub = 0;
-        --w;
-        continue;
-      }
-      if (phase == kGather) {  // y_k = prod_i y_k(base i), i = J[2] .. J[2] + gather - 1
-        if (sub >= (int)S.gather) {
-          store_elem(tbl + ((size_t)1 << k) * kW, x);
-          sub = 1;
-          if (++k > kCombH - 1) { phase = kCTab; k = 3; continue; }
-          load_elem(x, ygat + ((size_t)J[2] * (kCombH - 1) + (k - 1)) * kW);
-          continue;
-        }
-        ysrc = ygat + ((size_t)(J[2] + sub) * (kCombH - 1) + (k - 1)) * kW;
+      const uint32_t op = sched[pc++];
+      kind = op & ((1u << kOpShift) - 1u);
+      arg = op >> kOpShift;
+      if (kind == OP_END || kind == OP_SQR) break;
+      if (kind == OP_MUL_BASE) { ysrc = opaque_v(B); break; }
+      if (kind == OP_MUL_TBL) { ysrc = tbl + (size_t)arg * kW; break; }
+      if (kind == OP_MUL_WIN) {  // arg = w | o << 12
+        const uint32_t w = arg & 4095u;
+        const uint32_t byte = scalars[(size_t)J[1 + (arg >> 12)] * S.exp_bytes + (w >> 1)];
+        ysrc = tbl + (size_t)((w & 1) ? (byte & 15u) : (byte >> 4)) * kW;
         break;
       }
-      if (phase == kCTab) {  // entry k = (k & (k-1)) * (lowest bit of k)
-        while (k < (1 << kCombH) && (k & (k - 1)) == 0) ++k;
-        if (k >= (1 << kCombH)) { phase = kBegin; continue; }
-        load_elem(x, tbl + (size_t)(k & (k - 1)) * kW);
-        ysrc = tbl + (size_t)(k & -k) * kW;
+      if (kind == OP_MUL_COMB) { ysrc = tbl + (size_t)dig[arg] * kW; break; }
+      if (kind == OP_MUL_GATHER) {
+        ysrc = P.ygat + ((size_t)(J[2] + (arg >> 2)) * (kCombH - 1) + (arg & 3u)) * kW;
         break;
       }
-      if (phase == kTable) {
-        if (k < 16) { ysrc = B; break; }
-        phase = kBegin;
+      if (kind == OP_MUL_FB || kind == OP_LOAD_FB) {
+        const FbTab& T = (arg >> 10) ? fb1 : fb0;
+        const uint32_t kf = arg & 255u;
+        const uint32_t d = be_digit(scalars + (size_t)J[5 + 2 * ((arg >> 9) & 1u) + ((arg >> 8) & 1u)] * 32, 32,
+                                    kf * T.wbits, T.wbits);
+        const uint32_t* ent = T.data + ((size_t)(kf << T.wbits) + d) * kW;
+        if (kind == OP_MUL_FB) { ysrc = ent; break; }
+        load_elem(x, ent);
         continue;
       }
-      if (phase == kBegin) {
-        if (o >= S.nout) { done = true; break; }
-        if (S.has_base) {
-          e = scalars + (size_t)J[1 + o] * S.exp_bytes;
-          x_is_one = false;
-          if (comb) {
-            // column digits: bit j of each of the 5 rows (52 bits each)
+      switch (kind) {
+        case OP_LOAD_ONE: load_elem(x, opaque_s(C->one)); break;
+        case OP_LOAD_BASE: load_elem(x, opaque_v(B)); break;
+        case OP_LOAD_TBL: load_elem(x, tbl + (size_t)arg * kW); break;
+        case OP_LOAD_WIN: load_elem(x, tbl + (size_t)(scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4) * kW); break;
+        case OP_LOAD_COMB:
+          if constexpr (CT) {
+            ct_select_to_lds(slot, tbl, 1 << kCombH, dig[arg]);
+            wave_sync();
+            load_elem(x, slot);
+            wave_sync();
+          } else {
+            load_elem(x, tbl + (size_t)dig[arg] * kW);
+          }
+          break;
+        case OP_LOAD_GATHER: load_elem(x, P.ygat + ((size_t)J[2] * (kCombH - 1) + arg) * kW); break;
+        case OP_STORE_TBL: store_elem(tbl + (size_t)arg * kW, x); break;
+        case OP_STORE_Y:
+          if (P.yout != nullptr && live) store_elem(P.yout + ((size_t)gid * (kCombH - 1) + arg) * kW, x);
+          break;
+        case OP_STORE_R:
+          if (live) store_elem(P.rout + ((size_t)gid * 2 + arg) * kW, x);
+          break;
+        case OP_STORE_OUT:
+          if (live) store_elem(out + (size_t)J[3 + arg] * kW, x);
+          break;
+        case OP_EXP:
+          if (S.comb) {
+            // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each)
+            const uint8_t* e = scalars + (size_t)J[1 + arg] * 32;
             wave_sync();
             for (int j = glane(); j < kCombW; j += kT) {
               uint32_t d = 0;
@@ -518,80 +519,21 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
               dig[j] = (uint8_t)d;
             }
             wave_sync();
-            if constexpr (CT) {
-              ct_select_to_lds(slot, tbl, 1 << kCombH, dig[kCombW - 1]);
-              wave_sync();
-              load_elem(x, slot);
-              wave_sync();
-            } else {
-              load_elem(x, tbl + (size_t)dig[kCombW - 1] * kW);
-            }
-            w = kCombW - 2; sub = 0;
-            phase = kComb;
-          } else {
-            load_elem(x, tbl + (size_t)(e[0] >> 4) * kW);
-            w = 1; sub = 0;
-            phase = kVar;
           }
-        } else {
-          x_is_one = true;
-          t = 0; kf = 0;
-          phase = kFb;
-        }
-        continue;
+          break;
+        default: break;
       }
-      if (phase == kComb) {
-        if (w < 0) { t = 0; kf = 0; phase = kFb; continue; }
-        if (sub == 0) break;  // square
-        ysrc = tbl + (size_t)dig[w] * kW;
-#if EG_PREFETCH >= 2
-        if (!CT && w > 0) pf = tbl + (size_t)dig[w - 1] * kW;  // after the next squaring
-#endif
-        break;
-      }
-      if (phase == kVar) {
-        if (w >= nwin) { t = 0; kf = 0; phase = kFb; continue; }
-        if (sub < 4) break;  // square
-        const uint32_t byte = e[w >> 1];
-        const uint32_t d = (w & 1) ? (byte & 15u) : (byte >> 4);
-        ysrc = tbl + (size_t)d * kW;
-        break;
-      }
-      // kFb
-      if (t >= S.nfb[o]) {
-        if (x_is_one) load_elem(x, C->one);
-        if (gid < njobs) store_elem(out + (size_t)J[3 + o] * kW, x);
-        ++o;
-        phase = kBegin;
-        continue;
-      }
-      const FbTab& T = S.tab[o][t] ? fb1 : fb0;
-      if (kf >= T.nwin) { ++t; kf = 0; continue; }
-      const uint32_t d = be_digit(scalars + (size_t)J[5 + 2 * o + t] * 32, 32, kf * T.wbits, T.wbits);
-      const uint32_t* ent = T.data + ((size_t)(kf << T.wbits) + d) * kW;
-      if (x_is_one) { load_elem(x, ent); x_is_one = false; ++kf; continue; }
-      ysrc = ent;
-#if EG_PREFETCH
-      if (kf + 1 < T.nwin) {
-        const uint32_t d1 = be_digit(scalars + (size_t)J[5 + 2 * o + t] * 32, 32, (kf + 1) * T.wbits, T.wbits);
-        pf = T.data + ((size_t)((kf + 1) << T.wbits) + d1) * kW;
-      }
-#endif
-      break;
     }
-    if (done) break;
+    if (kind == OP_END) break;
     // ---- the one Montgomery multiply (or square) ----
     if (ysrc) {
       if constexpr (CT) {
-        if (phase == kComb) ct_select_to_lds(slot, tbl, 1 << kCombH, dig[w]);  // secret digit
+        if (kind == OP_MUL_COMB) ct_select_to_lds(slot, tbl, 1 << kCombH, dig[arg]);  // secret digit
         else elem_to_lds(slot, ysrc);
       } else {
         elem_to_lds(slot, ysrc);
       }
       wave_sync();
-#if EG_PREFETCH
-      if (pf) prefetch_elem(pf, pf_discard);
-#endif
       M.mul(x, slot);
     } else {
       regs_to_lds(slot, x);
@@ -599,27 +541,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       M.sqr(x, slot);
     }
     wave_sync();
-    // ---- bookkeeping ----
-    if (phase == kTable) { store_elem(tbl + (size_t)k * kW, x); ++k; }
-    else if (phase == kVar) { if (++sub == 5) { sub = 0; ++w; } }
-    else if (phase == kPre) {
-      ++k;
-      if (k % kCombW == 0) {
-        store_elem(tbl + ((size_t)1 << (k / kCombW)) * kW, x);
-        if (yout != nullptr && gid < njobs) store_elem(yout + ((size_t)gid * (kCombH - 1) + (k / kCombW - 1)) * kW, x);
-      }
-    }
-    else if (phase == kGather) { ++sub; }
-    else if (phase == kRsq) { ++k; }
-    else if (phase == kRc) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
-    else if (phase == kCTab) { store_elem(tbl + (size_t)k * kW, x); ++k; }
-    else if (phase == kComb) { if (sub == 0) sub = 1; else { sub = 0; --w; } }
-    else { ++kf; }
   }
-#if EG_PREFETCH
-  // no LDS-DMA write may land after the workgroup's LDS is handed to another workgroup
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
 }
 
 // ---------------------------------------------------------------------------------

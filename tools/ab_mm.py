@@ -21,7 +21,7 @@ def build(name, flags):
     BUILD.mkdir(exist_ok=True)
     out = BUILD / f"libeg_{name}.so"
     if not out.exists():
-        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
                "-Wno-unused-result", "-Wno-pass-failed", *flags.split(), "-I", str(ROOT / "include"), "-o", str(out),
                str(ROOT / "electionguard-remote_amd" / "csrc" / "eg_capi.hip")]
         subprocess.run(cmd, check=True)
