@@ -150,14 +150,21 @@ __global__ void __launch_bounds__(kBlock) k_import(const MontConsts* __restrict_
   uint32_t x[kL];
 #pragma unroll
   for (int j = 0; j < kL; ++j) x[j] = bits_limb(slot, kLimbBits * (glane() * kL + j));
-  if (lt_p != nullptr && glane() == 0) {
-    // lexicographic compare from the most significant word
+  if (lt_p != nullptr) {
+    // be < p: each lane compares its 128/kT words from the top; the most significant lane
+    // that differs decides
+    constexpr int kWords = 128 / kT;
     int cmp = 0;
-    for (int w = 127; w >= 0 && cmp == 0; --w) {
+#pragma unroll
+    for (int i = kWords - 1; i >= 0; --i) {
+      const int w = glane() * kWords + i;
       const uint32_t a = slot[w], b = C->pw[w];
-      cmp = a < b ? -1 : (a > b ? 1 : 0);
+      if (cmp == 0) cmp = a < b ? -1 : (a > b ? 1 : 0);
     }
-    if (gid < n) lt_p[gid] = cmp < 0 ? 1 : 0;
+    const uint32_t sh = gslot() * kT;
+    const uint32_t lt = (uint32_t)(__ballot(cmp < 0) >> sh) & ((1u << kT) - 1u);
+    const uint32_t ne = (uint32_t)(__ballot(cmp != 0) >> sh) & ((1u << kT) - 1u);
+    if (glane() == 0 && gid < n) lt_p[gid] = ne ? (uint8_t)((lt >> (31 - __builtin_clz(ne))) & 1u) : 0;
   }
   wave_sync();
   elem_to_lds(slot, C->r2);
@@ -166,30 +173,49 @@ __global__ void __launch_bounds__(kBlock) k_import(const MontConsts* __restrict_
   if (gid < n) store_elem(out + (size_t)gid * kW, x);
 }
 
-// Fully normalise a value held in the group slot (limbs in device format, value <= p)
-// by group-lane 0; maps p -> 0.  Then write 512 big-endian bytes.
-__device__ __forceinline__ void slot_normalize(const MontConsts* __restrict__ C, uint32_t* slot) {
-  if (glane() == 0) {
-    uint32_t carry = 0;
-    bool eq = true;
-    for (int a = 0; a < kN; ++a) {
-      const int ia = (a / kL) * kLP + (a % kL);
-      const uint32_t v = slot[ia] + carry;
-      const uint32_t l = v & kMask;
-      carry = v >> kLimbBits;
-      slot[ia] = l;
-      eq &= (l == C->p[ia]);
-    }
-    if (eq) {
-      for (int a = 0; a < kW; ++a) slot[a] = 0;
+// Canonical form of a value in [0, p] held in registers (this lane's kL limbs, limbs below
+// 2^b + 2^(64-2b) + 1 as mont_mul leaves them): limbs < 2^b, and p -> 0.  The kT lanes of the
+// group work in parallel: a local carry pass, then the carries between lanes ripple upward
+// (a carry crosses a lane only through saturated limbs, so one round nearly always settles
+// it; the loop runs until no lane receives a carry, at most kT rounds, and its exit is
+// wave-uniform), then a group-wide equality test against p's limbs.
+template <bool F>
+__device__ __forceinline__ void regs_normalize(const Mont<F>& M, uint32_t (&x)[kL]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) {
+    const uint32_t v = x[j] + c;
+    x[j] = v & kMask;
+    c = v >> kLimbBits;
+  }
+  const bool g0 = glane() == 0;
+  for (int round = 0; round < kT; ++round) {
+    uint32_t cin = from_prev(c);  // carry out of the lane below (the group's top carry is 0: value < R)
+    if (g0) cin = 0;
+    if (__ballot(cin != 0) == 0) break;
+    c = 0;
+    if (cin) {
+#pragma unroll
+      for (int j = 0; j < kL; ++j) {
+        const uint32_t v = x[j] + cin;
+        x[j] = v & kMask;
+        cin = v >> kLimbBits;
+      }
+      c = cin;
     }
   }
-  wave_sync();
+  bool eq = true;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) eq &= x[j] == M.p[j];
+  const uint64_t gmask = (uint64_t)((1u << kT) - 1u) << (gslot() * kT);
+  if ((__ballot(!eq) & gmask) == 0) {
+#pragma unroll
+    for (int j = 0; j < kL; ++j) x[j] = 0;
+  }
 }
 
-__device__ __forceinline__ void slot_to_be(const MontConsts* __restrict__ C, uint32_t* slot,
-                                           uint8_t* __restrict__ dst, bool do_store) {
-  slot_normalize(C, slot);
+// 512 big-endian bytes of a canonical value held in the group slot (regs_normalize'd).
+__device__ __forceinline__ void slot_to_be(uint32_t* slot, uint8_t* __restrict__ dst, bool do_store) {
   constexpr int kPer = 128 / kT;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -221,16 +247,17 @@ __global__ void __launch_bounds__(kBlock) k_export(const MontConsts* __restrict_
   wave_sync();
   M.mul(x, slot);  // leave the Montgomery domain: value in [0, p]
   wave_sync();
+  regs_normalize(M, x);
   regs_to_lds(slot, x);
   wave_sync();
-  slot_to_be(C, slot, be + (size_t)gid * 512, gid < n);
+  slot_to_be(slot, be + (size_t)gid * 512, gid < n);
 }
 
 // Residue (subgroup) test of n bases from their k_pow residue pairs (PowShape::resid):
 //   pair i = (z, w) = (B^(2^256), B^c) in Montgomery form;  B^q == 1  <=>  z == w and B != 0
 // (B^(2^256) = B^q * B^c, and B is invertible unless B == 0, where z = w = 0).
 // flags[i * fstride] &= verdict — the per-element range flag of the verifier (k_import).
-// Cost: 2 MM (leaving the Montgomery domain) + two serial normalisations per base.
+// Cost: 2 MM (leaving the Montgomery domain) + two lane-parallel normalisations per base.
 template <bool F>
 __global__ void __launch_bounds__(kBlock) k_resid_check(const MontConsts* __restrict__ C,
                                                         const uint32_t* __restrict__ pairs, uint32_t n,
@@ -249,18 +276,14 @@ __global__ void __launch_bounds__(kBlock) k_resid_check(const MontConsts* __rest
     wave_sync();
     M.mul(x, slot);  // value in [0, p]
     wave_sync();
-    regs_to_lds(slot, x);
-    wave_sync();
-    slot_normalize(C, slot);  // canonical limbs, p -> 0
-    const uint32_t* s = slot + glane() * kLP;
+    regs_normalize(M, x);  // canonical limbs, p -> 0
     if (h == 0) {
 #pragma unroll
-      for (int j = 0; j < kL; ++j) { z[j] = s[j]; nz |= z[j] != 0; }
+      for (int j = 0; j < kL; ++j) { z[j] = x[j]; nz |= z[j] != 0; }
     } else {
 #pragma unroll
-      for (int j = 0; j < kL; ++j) eq &= z[j] == s[j];
+      for (int j = 0; j < kL; ++j) eq &= z[j] == x[j];
     }
-    wave_sync();
   }
   const uint64_t neq = __ballot(!eq), nzb = __ballot(nz);
   const uint64_t gmask = (uint64_t)((1u << kT) - 1u) << (gslot() * kT);
