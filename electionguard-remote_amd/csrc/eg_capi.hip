@@ -158,6 +158,9 @@ struct eg_ctx {
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
   std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
+  // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
+  // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
+  size_t pow_slots = 0;
   // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
   // most recently used first
   std::vector<std::pair<std::array<uint8_t, 512>, eg_fixed_base*>> share_keys;
@@ -337,12 +340,16 @@ static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const
 // later gather launch; ygat: the y_k array a gather launch (S.gather > 0) multiplies together.
 // tail (optional): a second, independent job population (shape tail->S) appended to the LAST
 // sub-launch so its short jobs fill that launch's tail (PowPart in eg_kernels.hpp).
+// jobs per k_pow sub-launch (bounds the per-launch scratch: 32 comb entries per job)
+constexpr size_t kPowMaxJobs = (size_t)1 << 18;
+
 struct PowTail {
   PowShape S;
   const uint32_t* jobs;
   size_t njobs;
   uint32_t* yout;
   const uint32_t* ygat;
+  uint32_t* rout;  // residue pairs (tail->S.resid)
 };
 static size_t pow_scratch_per_group(const PowShape& S) {
   return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
@@ -360,12 +367,14 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
   if (tail && tail->S.gather && (!tail->S.comb || !tail->ygat))
     return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
+  if (tail && tail->S.resid && (!tail->S.comb || tail->S.gather || !tail->rout))
+    return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
   if (tail && !tail->njobs) tail = nullptr;
   if (!njobs && !tail) return EG_OK;
   const size_t per = pow_scratch_per_group(S);
   const size_t per1 = tail ? pow_scratch_per_group(tail->S) : 0;
   // bound the per-launch scratch (table of 16/32 powers per job)
-  const size_t max_jobs = (size_t)1 << 18;
+  const size_t max_jobs = kPowMaxJobs;
   MMCount mm_job, mm_tail;
   const uint32_t *sched = nullptr, *sched_tail = nullptr;
   int src = pow_schedule_dev(c, S, f0, f1, &sched, &mm_job);
@@ -384,7 +393,7 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     PowPart P1{};
     if (nt) {
       P1 = PowPart{tail->S, sched_tail, tail->jobs, (uint32_t)nt, grid_for(nt),
-                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, nullptr, nullptr};
+                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, tail->rout, nullptr};
     }
     ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
@@ -559,6 +568,13 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
       if ((c->h.qc[b >> 5] >> (b & 31)) & 1u) { c->h.qc_bits = (uint32_t)b + 1; break; }
   }
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
+  {
+    int cus = 0, per_cu = 0;
+    const char* ts = getenv("EG_TAIL_SPLIT");
+    if (!(ts && ts[0] == '0') && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pow<true, false>, kBlock, 0) == hipSuccess)
+      c->pow_slots = (size_t)cus * (size_t)per_cu;
+  }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;

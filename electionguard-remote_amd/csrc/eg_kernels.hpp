@@ -84,20 +84,6 @@ __device__ __forceinline__ uint32_t group_id() { return blockIdx.x * kGroupsPerB
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
-// A copy of a loop-invariant pointer that the compiler cannot see through: loads from it stay
-// where they are written instead of being hoisted out of k_pow's op loop and held in VGPRs
-// across every multiply (v: per-lane pointer, s: wave-uniform pointer).
-template <class T>
-__device__ __forceinline__ T* opaque_v(T* q) {
-  asm volatile("" : "+v"(q));
-  return q;
-}
-template <class T>
-__device__ __forceinline__ T* opaque_s(T* q) {
-  asm volatile("" : "+s"(q));
-  return q;
-}
-
 // x <- x * x
 template <bool F>
 __device__ __forceinline__ void msqr(const Mont<F>& M, uint32_t (&x)[kL], uint32_t* slot) {
@@ -467,9 +453,6 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   // Outer loop: one Montgomery multiply (or square) per trip, at a single inlined site; the
   // inner loop runs the program's loads, stores and digit spreads up to the next multiply.
   uint32_t pc = 0;
-#ifdef EG_XINIT
-  load_elem(x, C->one);
-#endif
   while (true) {
     const uint32_t* ysrc = nullptr;  // nullptr: square
     uint32_t kind = OP_END, arg = 0;
@@ -478,7 +461,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       kind = op & ((1u << kOpShift) - 1u);
       arg = op >> kOpShift;
       if (kind == OP_END || kind == OP_SQR) break;
-      if (kind == OP_MUL_BASE) { ysrc = opaque_v(B); break; }
+      if (kind == OP_MUL_BASE) { ysrc = B; break; }
       if (kind == OP_MUL_TBL) { ysrc = tbl + (size_t)arg * kW; break; }
       if (kind == OP_MUL_WIN) {  // arg = w | o << 12
         const uint32_t w = arg & 4095u;
@@ -502,8 +485,8 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         continue;
       }
       switch (kind) {
-        case OP_LOAD_ONE: load_elem(x, opaque_s(C->one)); break;
-        case OP_LOAD_BASE: load_elem(x, opaque_v(B)); break;
+        case OP_LOAD_ONE: load_elem(x, C->one); break;
+        case OP_LOAD_BASE: load_elem(x, B); break;
         case OP_LOAD_TBL: load_elem(x, tbl + (size_t)arg * kW); break;
         case OP_LOAD_WIN: load_elem(x, tbl + (size_t)(scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4) * kW); break;
         case OP_LOAD_COMB:

@@ -122,6 +122,8 @@ if __name__ == "__main__":
         env_extra = {}
         if name.endswith("@nocomb"):
             env_extra["EG_NO_COMB"] = "1"
+        if name.endswith("@notail"):
+            env_extra["EG_TAIL_SPLIT"] = "0"
         lib = build(name.split("@")[0], flags)
         nb = int(os.environ.get("AB_NB", "4000"))
         if mode == "verify":
