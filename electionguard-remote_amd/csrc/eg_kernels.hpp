@@ -862,11 +862,14 @@ __global__ void __launch_bounds__(kBlock) k_hash_check(const uint8_t* __restrict
                                                        const uint8_t* __restrict__ pre_ok2, uint32_t pre2_div,
                                                        uint8_t* __restrict__ ok, uint8_t* __restrict__ out_h,
                                                        uint32_t hash_minimal) {
-  __shared__ uint32_t s_buf[kBlock * 16];
+  // one 64-B block buffer per thread, at a 68-B stride: with a 64-B stride every lane's
+  // byte k sits in the same LDS bank and each buffer access is a 32-way conflict
+  constexpr int kBufStride = 17;
+  __shared__ uint32_t s_buf[kBlock * kBufStride];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Sha256 H;
-  H.init(s_buf + threadIdx.x * 16);
+  H.init(s_buf + threadIdx.x * kBufStride);
   H.put('|');
   H.put_hex(qbar_be, 32, hash_minimal != 0);
   H.put('|');
