@@ -248,3 +248,26 @@ def test_oversized_arguments_rejected(group):
     assert rc == 1 and b"manifest" in lib.eg_last_error()
     rc = lib.eg_encrypt_ballots(group.handle, one, 1, 1 << 11, 1 << 10, one, one, one, one, one, one)
     assert rc == 1 and b"manifest" in lib.eg_last_error()
+
+
+@pytest.mark.parametrize("slots", ["0", "37", "100", "768", "5000"])
+def test_launch_split_independent(group, slots, monkeypatch):
+    """The verifier sizes its three k_pow launches from the resident-workgroup count (beta
+    head in launch 1, contest-a jobs split between launches 2 and 3; eg_capi_ballot.inc).
+    Verdicts and tally must not depend on where the splits fall: EG_POW_SLOTS forces other
+    split points (0 = no split), against the CPython tally and a tamper in the moved jobs."""
+    from electionguard.ballot import EncryptedBallots, Manifest, Verifier
+    man = Manifest(4, 5, 1)
+    nb = 700  # 16,800 selection jobs = 525 workgroups: every slot count above splits differently
+    key, K, qbar, eb = _encrypt(group, man, nb, 91)
+    V = Verifier(group, key, qbar, man)
+    monkeypatch.setenv("EG_POW_SLOTS", slots)
+    ok_s, ok_c, tally = V.verify(eb)
+    assert ok_s.all() and ok_c.all()
+    assert np.array_equal(tally, _tally_products(man, eb))
+    rp, cp = eb.rproof.copy(), eb.cproof.copy()
+    rp[3, 7, 2, 4] ^= 0x08       # a beta-head job (ballot 3) in launch 1 when split
+    cp[650, 1, 1, 9] ^= 0x20     # a late contest-a job (launch 3 when split)
+    ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, cp), with_tally=False)
+    assert np.argwhere(~ok_s).tolist() == [[3, 7]]
+    assert np.argwhere(~ok_c).tolist() == [[650, 1]]
