@@ -95,10 +95,14 @@ def main():
     votes = random_votes(rng, man, nb)
     sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
     cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    eb = batch_encryption(group, key, qbar, man, votes, sn, cn)  # the ballots the step verifies
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    eb = batch_encryption(group, key, qbar, man, votes, sn, cn)
-    enc_s = time.perf_counter() - t
+    enc_s = None
+    for _ in range(2):  # host-pointer encryption rate: best of two warm calls (same nonces, same bytes)
+        t = time.perf_counter()
+        batch_encryption(group, key, qbar, man, votes, sn, cn)
+        dt = time.perf_counter() - t
+        enc_s = dt if enc_s is None else min(enc_s, dt)
 
     dev = torch.device("cuda", local)
     d_cts = torch.from_numpy(eb.cts).to(dev)
@@ -243,7 +247,7 @@ def config_name(contests: int, selections: int, nb: int, world: int) -> str:
     return f"custom manifest {contests}x{selections}, {nb} ballots per GPU x {gpus}"
 
 
-def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2):
+def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=5):
     """batch-encrypt with votes, nonces and outputs resident in HBM (eg_encrypt_ballots_dev),
     best of `reps` timed runs; the outputs must equal the host-pointer encryption's bytes
     (same injected nonces) already resident in d_cts / d_rp / d_cp."""
