@@ -24,15 +24,17 @@ __device__ __constant__ const uint32_t kSha256K[64] = {
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
 struct Sha256 {
-  uint32_t* buf;  // 16 words of LDS owned by this thread
+  uint32_t* buf;  // 16 words of LDS owned by this thread (the current 64-byte block)
   uint32_t h[8];
-  uint32_t len;
+  uint32_t len;   // bytes so far
+  uint32_t pend;  // the block word being filled: bytes [len & ~3, len) in its low bytes
 
   __device__ __forceinline__ void init(uint32_t* lds_words) {
     buf = lds_words;
     h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
     h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
     len = 0;
+    pend = 0;
   }
 
   __device__ void compress() {
@@ -63,25 +65,62 @@ struct Sha256 {
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
   }
 
+  // one byte
   __device__ __forceinline__ void put(uint32_t ch) {
-    reinterpret_cast<uint8_t*>(buf)[len & 63] = (uint8_t)ch;
+    pend |= (ch & 0xFFu) << (8 * (len & 3));
     ++len;
-    if ((len & 63) == 0) compress();
+    if ((len & 3) == 0) {
+      buf[((len >> 2) - 1) & 15] = pend;
+      pend = 0;
+      if ((len & 63) == 0) compress();
+    }
+  }
+
+  // four bytes at once (v's low byte first): one LDS word store instead of four byte stores;
+  // at a byte offset k = len & 3 the first 4 - k bytes complete the pending word
+  __device__ __forceinline__ void put4(uint32_t v) {
+    const uint32_t k = len & 3, wi = (len >> 2) & 15;
+    if (k == 0) {
+      buf[wi] = v;
+    } else {
+      buf[wi] = pend | (v << (8 * k));
+      pend = v >> (32 - 8 * k);
+    }
+    len += 4;
+    if (wi == 15) compress();
   }
 
   __device__ __forceinline__ static uint32_t hexc(uint32_t v) { return v < 10 ? ('0' + v) : ('A' + v - 10); }
 
-  // upper-case hex of n big-endian bytes (n multiple of 16, 16-B aligned source)
-  // Upper-case hex of n big-endian bytes.  minimal = false: fixed width (2n chars);
+  // four nibbles (one per byte, 0..15) -> four upper-case hex characters, bytewise SWAR
+  __device__ __forceinline__ static uint32_t hex4(uint32_t n) {
+    const uint32_t ge10 = ((n + 0x06060606u) >> 4) & 0x01010101u;  // nibble >= 10
+    return n + 0x30303030u + (ge10 << 3) - ge10;                     // '0' + n (+ 7 for A-F)
+  }
+
+  // Upper-case hex of n big-endian bytes.  minimal = false: fixed width (2n chars, n a
+  // multiple of 16, 16-B aligned source), 8 characters per source word through put4;
   // minimal = true: leading zero BYTES dropped, at least one kept (the integer's even-length
-  // hex, e.g. 0 -> "00", 0xABC -> "0ABC": electionguard-python 1.x to_hex); see
-  // eg_ctx_set_hash_format.
+  // hex, e.g. 0 -> "00", 0xABC -> "0ABC": electionguard-python 1.x to_hex), a byte at a
+  // time; see eg_ctx_set_hash_format.
   __device__ void put_hex(const uint8_t* __restrict__ p, uint32_t n, bool minimal = false) {
     const uint4* s = reinterpret_cast<const uint4*>(p);
-    uint32_t first = 0;
-    if (minimal) {
-      while (first + 1 < n && p[first] == 0) ++first;
+    if (!minimal) {
+      for (uint32_t i = 0; i < n / 16; ++i) {
+        const uint4 v = s[i];
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lo = ws[k] & 0x0F0F0F0Fu, hi = (ws[k] >> 4) & 0x0F0F0F0Fu;
+          // bytes b0..b3 in memory order -> characters hi(b0) lo(b0) hi(b1) lo(b1) | hi(b2) ...
+          put4(hex4(__builtin_amdgcn_perm(hi, lo, 0x01050004u)));
+          put4(hex4(__builtin_amdgcn_perm(hi, lo, 0x03070206u)));
+        }
+      }
+      return;
     }
+    uint32_t first = 0;
+    while (first + 1 < n && p[first] == 0) ++first;
     for (uint32_t i = first / 16; i < n / 16; ++i) {
       const uint4 v = s[i];
       const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
