@@ -114,6 +114,8 @@ struct ProfRec {
   hipEvent_t a, b;
   double mm;   // Montgomery operations (multiplies + squarings)
   double sqr;  // of which squarings (symmetric-half schedule)
+  uint64_t* d_clk = nullptr;  // per workgroup (shader cycles, wall ticks) of the launch (k_pow clk)
+  uint32_t nblocks = 0;
 };
 
 // Montgomery operations of one k_pow job, split into squarings and multiplies: counted from
@@ -161,6 +163,7 @@ struct eg_ctx {
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
   // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
   size_t pow_slots = 0;
+  double prof_clock_ghz = 0;  // shader clock over the last profiled k_pow launches (eg_ctx_profile_clock)
   // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
   // most recently used first
   std::vector<std::pair<std::array<uint8_t, 512>, eg_fixed_base*>> share_keys;
@@ -397,18 +400,21 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     }
     ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
+    const dim3 grid(P0.nblocks + P1.nblocks);
     if (c->timing) {
       HIPCHK(hipEventCreate(&pr.a));
       HIPCHK(hipEventCreate(&pr.b));
+      HIPCHK(hipMalloc(&pr.d_clk, (size_t)grid.x * 2 * sizeof(uint64_t)));
+      pr.nblocks = grid.x;
       HIPCHK(hipEventRecord(pr.a, c->stream));
     }
-    const dim3 grid(P0.nblocks + P1.nblocks);
+    uint64_t* clk = pr.d_clk;
     if (c->h.friendly) {
-      if (ct) hipLaunchKernelGGL((k_pow<true, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
-      else hipLaunchKernelGGL((k_pow<true, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+      if (ct) hipLaunchKernelGGL((k_pow<true, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
+      else hipLaunchKernelGGL((k_pow<true, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
     } else {
-      if (ct) hipLaunchKernelGGL((k_pow<false, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
-      else hipLaunchKernelGGL((k_pow<false, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1);
+      if (ct) hipLaunchKernelGGL((k_pow<false, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
+      else hipLaunchKernelGGL((k_pow<false, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
     }
     HIPCHK(hipGetLastError());
     if (c->timing) {
@@ -622,6 +628,11 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
   for (auto& kv : c->cache)
     if (kv.second.ptr) hipFree(kv.second.ptr);
   for (auto& kv : c->sched) hipFree(const_cast<uint32_t*>(kv.second.ptr));
+  for (auto& r : c->prof) {  // a profile window left open
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+    if (r.d_clk) hipFree(r.d_clk);
+  }
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);
@@ -808,12 +819,21 @@ extern "C" int eg_prod_reduce(eg_ctx* c, const uint8_t* elems_be, size_t groups,
 extern "C" int eg_ctx_profile_begin(eg_ctx* c) {
   if (!c) return fail(EG_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipStreamSynchronize(c->stream));  // a pending window's launches may still write d_clk
   for (auto& r : c->prof) {
     hipEventDestroy(r.a);
     hipEventDestroy(r.b);
+    if (r.d_clk) hipFree(r.d_clk);
   }
   c->prof.clear();
   c->timing = true;
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_profile_clock(eg_ctx* c, double* ghz) {
+  if (!c || !ghz) return fail(EG_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *ghz = c->prof_clock_ghz;
   return EG_OK;
 }
 
@@ -822,16 +842,30 @@ extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  double t = 0, m = 0, sq = 0;
+  double t = 0, m = 0, sq = 0, cyc = 0, wall = 0;
   for (auto& r : c->prof) {
     float x = 0;
     HIPCHK(hipEventElapsedTime(&x, r.a, r.b));
     t += x;
     m += r.mm;
     sq += r.sqr;
+    if (r.d_clk) {
+      std::vector<uint64_t> h((size_t)r.nblocks * 2);
+      HIPCHK(hipMemcpy(h.data(), r.d_clk, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      for (uint32_t b = 0; b < r.nblocks; ++b) {
+        cyc += (double)h[2 * b];
+        wall += (double)h[2 * b + 1];
+      }
+      hipFree(r.d_clk);
+    }
     hipEventDestroy(r.a);
     hipEventDestroy(r.b);
   }
+  int wall_khz = 0;
+  c->prof_clock_ghz = 0;
+  if (wall > 0 && hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess &&
+      wall_khz > 0)
+    c->prof_clock_ghz = cyc / (wall / ((double)wall_khz * 1e3)) / 1e9;
   if (ms) *ms = t;
   if (mm) *mm = m;
   if (sqr) *sqr = sq;

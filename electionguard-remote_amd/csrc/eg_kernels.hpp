@@ -426,8 +426,12 @@ template <bool F, bool CT>
 __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowPart P0,
                                                 PowPart P1, const uint32_t* __restrict__ elems,
                                                 const uint8_t* __restrict__ scalars,
-                                                uint32_t* __restrict__ out, FbTab fb0, FbTab fb1) {
+                                                uint32_t* __restrict__ out, FbTab fb0, FbTab fb1,
+                                                uint64_t* __restrict__ clk) {
   __shared__ uint8_t s_dig[kGroupsPerBlock][64];
+  // clk (profiling only): per workgroup, shader-clock cycles and constant-rate wall ticks
+  // from its start to its end, so the host can report the clock the launch ran at
+  const uint64_t cyc0 = clk ? clock64() : 0, wall0 = clk ? wall_clock64() : 0;
   const bool second = blockIdx.x >= P0.nblocks;
   const PowPart& P = second ? P1 : P0;  // kernarg memory: shape fields stay scalar loads
   const PowShape& S = P.S;
@@ -547,6 +551,10 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       M.sqr(x, slot);
     }
     wave_sync();
+  }
+  if (clk && threadIdx.x == 0) {
+    clk[2 * (size_t)blockIdx.x] = clock64() - cyc0;
+    clk[2 * (size_t)blockIdx.x + 1] = wall_clock64() - wall0;
   }
 }
 

@@ -71,6 +71,7 @@ class KernelProfile:
     mont_ops: float    # Montgomery multiplies + squarings
     squarings: float   # of which squarings
     launches: int
+    clock_ghz: float = 0.0  # shader clock the launches ran at (per-workgroup clock64 / wall_clock64)
 
     @property
     def macs(self) -> float:
@@ -230,7 +231,9 @@ class GroupContext:
         native.check(self._lib, "eg_ctx_profile_end",
                      self._lib.eg_ctx_profile_end(self._ctx, ctypes.byref(ms), ctypes.byref(mm), ctypes.byref(sq),
                                                   ctypes.byref(n)))
-        return KernelProfile(ms.value, mm.value, sq.value, n.value)
+        ghz = ctypes.c_double()
+        native.check(self._lib, "eg_ctx_profile_clock", self._lib.eg_ctx_profile_clock(self._ctx, ctypes.byref(ghz)))
+        return KernelProfile(ms.value, mm.value, sq.value, n.value, ghz.value)
 
     def sync(self) -> None:
         native.check(self._lib, "eg_ctx_sync", self._lib.eg_ctx_sync(self._ctx))

@@ -18,7 +18,7 @@ LIB_PATH = LIB_DIR / "libeg_hip.so"
 # Every symbol declared in include/eg_hip.h (tests check the library exports them).
 EXPORTED = [
     "eg_last_error", "eg_version", "eg_ctx_create", "eg_ctx_destroy", "eg_ctx_sync",
-    "eg_ctx_profile_begin", "eg_ctx_profile_end", "eg_ctx_g_table", "eg_ctx_set_hash_format",
+    "eg_ctx_profile_begin", "eg_ctx_profile_end", "eg_ctx_profile_clock", "eg_ctx_g_table", "eg_ctx_set_hash_format",
     "eg_fixed_base_create", "eg_fixed_base_destroy", "eg_powp_batch", "eg_fb_pow_batch",
     "eg_powp_batch_dev", "eg_fb_pow_batch_dev",
     "eg_multp_batch", "eg_prod_reduce", "eg_multinv_batch", "eg_verify_ballots",
@@ -58,6 +58,7 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_ctx_sync": ([P], I),
         "eg_ctx_profile_begin": ([P], I),
         "eg_ctx_profile_end": ([P, D, D, D, ctypes.POINTER(I)], I),
+        "eg_ctx_profile_clock": ([P, D], I),
         "eg_ctx_g_table": ([P], P),
         "eg_ctx_set_hash_format": ([P, I], I),
         "eg_fixed_base_create": ([P, P, I, ctypes.POINTER(c_vp)], I),

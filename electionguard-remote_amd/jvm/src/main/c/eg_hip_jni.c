@@ -84,12 +84,13 @@ JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_profileBegin(JNIEnv* env, jc
 }
 
 JNIEXPORT jdoubleArray JNICALL Java_electionguard_gpu_EgHip_profileEnd(JNIEnv* env, jclass cls, jlong ctx) {
-  double v[4] = {0, 0, 0, 0};
+  double v[5] = {0, 0, 0, 0, 0};
   int launches = 0;
   if (check_rc(env, eg_ctx_profile_end((eg_ctx*)(intptr_t)ctx, &v[0], &v[1], &v[2], &launches))) return NULL;
   v[3] = (double)launches;
-  jdoubleArray out = (*env)->NewDoubleArray(env, 4);
-  if (out) (*env)->SetDoubleArrayRegion(env, out, 0, 4, v);
+  if (check_rc(env, eg_ctx_profile_clock((eg_ctx*)(intptr_t)ctx, &v[4]))) return NULL;
+  jdoubleArray out = (*env)->NewDoubleArray(env, 5);
+  if (out) (*env)->SetDoubleArrayRegion(env, out, 0, 5, v);
   return out;
 }
 

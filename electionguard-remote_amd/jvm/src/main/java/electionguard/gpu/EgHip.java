@@ -37,7 +37,7 @@ public final class EgHip {
 
   public static native void profileBegin(long ctx);
 
-  /** @return {kernel ms, Montgomery ops, of which squarings, launches} of the dominant kernel. */
+  /** @return {kernel ms, Montgomery ops, of which squarings, launches, shader clock GHz} of the dominant kernel. */
   public static native double[] profileEnd(long ctx);
 
   /** The fixed-base table of g built at ctxCreate (owned by the context: do not destroy). */

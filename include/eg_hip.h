@@ -76,6 +76,10 @@ int eg_ctx_sync(eg_ctx* ctx);
  * Any out pointer may be NULL. */
 int eg_ctx_profile_begin(eg_ctx* ctx);
 int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_ops, double* squarings, int* launches);
+/* Shader clock (GHz) the k_pow launches of the last profile_begin/end window ran at: each
+ * workgroup's clock64() cycles over its wall_clock64() ticks, summed over workgroups
+ * (0 when nothing was profiled).  Instrumentation; no reference counterpart. */
+int eg_ctx_profile_clock(eg_ctx* ctx, double* ghz);
 /* Fixed-base table for g (built at ctx creation) — accessor. */
 eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
 

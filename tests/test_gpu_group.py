@@ -138,3 +138,20 @@ def test_powp_and_fb_dev_pointers(group, oracle_group):
     for i in range(33):
         assert be2i(out[i]) == O.powP(bases[20], exps[i]), i
     fb.close()
+
+
+def test_profile_counts_and_clock(group):
+    """eg_ctx_profile_end counts the k_pow work of the window from the op programs, and
+    eg_ctx_profile_clock reports the shader clock it ran at (per-workgroup clock64 over
+    wall_clock64 ticks): a 4-bit-window powP is 14 table MMs + 63 x (4 sq + 1 mul)."""
+    rng = np.random.default_rng(5)
+    n = 4096
+    bases = rng.integers(0, 256, size=(n, 512), dtype=np.uint8)
+    bases[:, 0] = 0
+    exps = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    group.profile_begin()
+    group.powP_batch(bases, exps)
+    kp = group.profile_end()
+    assert kp.launches == 1
+    assert kp.mont_ops == n * (14 + 63 * 5) and kp.squarings == n * 63 * 4
+    assert kp.ms > 0 and 0.5 < kp.clock_ghz < 3.5, kp
