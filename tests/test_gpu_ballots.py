@@ -130,3 +130,42 @@ def test_encrypt_verify_roundtrip_random(group):
     prs = [O.RangeProof(*[I(eb.rproof[b, i, k]) for k in range(4)]) for i in range(man.nsel)]
     cps = [O.GenericProof(I(eb.cproof[b, c, 0]), I(eb.cproof[b, c, 1])) for c in range(man.n_contests)]
     assert O.verify_ballot(og, K, qbar, O.Manifest(4, 5, 1), O.EncryptedBallot(cts, prs, cps))
+
+
+def test_window_path_context_matches_comb(group, monkeypatch):
+    """EG_NO_COMB=1 (read at context creation) runs the gathered contest jobs and the trustee
+    shares through the 4-bit fixed-window programs instead of the Lim-Lee comb: a second
+    context built that way must give the same verdicts, tally, tamper flags and trustee
+    shares as the default one (and the oracle's tally)."""
+    from electionguard.ballot import ElectionKey, EncryptedBallots, Manifest, Verifier
+    from electionguard.core import GroupContext
+    from electionguard.decrypt import partial_decrypt_batch
+    og, rng, K, qbar, key = _setup(group, seed=41)
+    man = Manifest(2, 3, 1)
+    cts, rp, cp, obs = _oracle_ballots(og, K, qbar, O.Manifest(2, 3, 1), 5, rng)
+    eb = EncryptedBallots(cts, rp, cp)
+    monkeypatch.setenv("EG_NO_COMB", "1")
+    g2 = GroupContext(group.p, group.q, group.g, device=group.device)
+    monkeypatch.delenv("EG_NO_COMB")
+    try:
+        key2 = ElectionKey(g2, K)
+        s1, c1, t1 = Verifier(group, key, qbar, man).verify(eb)
+        s2, c2, t2 = Verifier(g2, key2, qbar, man).verify(eb)
+        assert s1.all() and c1.all() and (s2 == s1).all() and (c2 == c1).all() and (t2 == t1).all()
+        want = O.accumulate_tally(og, O.Manifest(2, 3, 1), [e for _, e in obs])
+        for s, ct in enumerate(want):
+            assert be2i(t2[s, 0]) == ct.pad and be2i(t2[s, 1]) == ct.data, s
+        cp2 = cp.copy()
+        cp2[3, 1, 1, 7] ^= 0x40
+        s3, c3, _ = Verifier(g2, key2, qbar, man).verify(EncryptedBallots(cts, rp, cp2), with_tally=False)
+        assert s3.all() and np.argwhere(~c3).tolist() == [[3, 1]]
+        texts = np.ascontiguousarray(cts[:, :, :, :].reshape(-1, 2, 512)[:7])
+        secret = rng.randrange(og.q)
+        nonces = np.stack([np.frombuffer(rng.randrange(og.q).to_bytes(32, "big"), np.uint8) for _ in range(7)])
+        Ma, pa = partial_decrypt_batch(group, secret, qbar, texts, nonces)
+        Mb, pb = partial_decrypt_batch(g2, secret, qbar, texts, nonces)
+        assert np.array_equal(Ma, Mb) and np.array_equal(pa, pb)
+        for i in range(7):
+            assert be2i(Ma[i]) == pow(be2i(texts[i, 0]), secret, og.p)
+    finally:
+        g2.close()
