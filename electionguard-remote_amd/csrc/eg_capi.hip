@@ -219,9 +219,13 @@ static int launch_export(eg_ctx* c, const uint32_t* d_in, size_t n, uint8_t* d_b
 //   window     : table B^0..B^15 (14 MM); per exponent MSB-first 4-bit windows, 4 sq + 1 mul
 //   comb       : y_k = B^(2^(52k)) (208 sq, kept in yout for gather jobs), the 32 subset
 //                products (26 MM), per exponent 51 x (1 sq + 1 mul) from column digits
+//   comb, v = 2: the chain also keeps B^(2^(52r+26)) (to 2^234), two subset tables (52 MM), per
+//                exponent 25 x (1 sq + 2 mul): 26 MM fewer per pair when the chain is paid anyway
 //   gather     : y_k = prod of the factor jobs' y_k (4 x (gather-1) MM instead of 208 sq)
-//   resid      : 48 more squarings past y_4 give z = B^(2^256); w = B^c by a left-to-right
-//                ladder over the public c = 2^256 - q; both to rout (k_resid_check: z == w)
+//   resid      : the chain runs on to z = B^(2^256); w = B^c for the public c = 2^256 - q is the
+//                product of the chain's B^(2^k) at c's set bits (kept in free table slots while
+//                the chain passes them: popcount(c) - 1 MM, 5 for EG's c = 189), or a
+//                left-to-right ladder when c has too many bits; both to rout (k_resid_check)
 //   fixed base : radix-table windows of g / K per term; the first one loads instead of multiplying
 static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S, const FbTab& f0, const FbTab& f1,
                                           MMCount* mm) {
@@ -233,9 +237,11 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
     else if (k != OP_END && k <= kOpMulLast) n.mul += 1;
   };
   const bool comb = S.comb != 0;
+  const uint32_t nb = (comb && S.blocks == 2) ? 2u : 1u;  // Lim-Lee column blocks
+  const uint32_t bw = (uint32_t)kCombW / nb;             // columns per block
   if (S.has_base && !(comb && S.shared_comb)) {
     op(OP_LOAD_ONE);
-    op(OP_STORE_TBL, 0);
+    for (uint32_t t = 0; t < nb; ++t) op(OP_STORE_TBL, t << kCombH);
     op(OP_LOAD_BASE);
     op(OP_STORE_TBL, 1);
     if (!comb) {
@@ -251,29 +257,59 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
           op(OP_STORE_TBL, 1u << k);
         }
       } else {
-        for (uint32_t k = 1; k <= (uint32_t)((kCombH - 1) * kCombW); ++k) {
-          op(OP_SQR);
-          if (k % kCombW == 0) {
-            op(OP_STORE_TBL, 1u << (k / kCombW));
-            op(OP_STORE_Y, k / kCombW - 1);
+        // residue test: c's set bits k >= 1 take table-0 slots that are not comb bases (the
+        // composite indices, free until the subset products below)
+        std::vector<uint32_t> cslot(256, 0);
+        bool chain_c = false;
+        if (S.resid) {
+          uint32_t pc = 0;
+          for (uint32_t k = 1; k < H.qc_bits && k < 256; ++k) pc += (H.qc[k >> 5] >> (k & 31)) & 1u;
+          chain_c = H.qc_bits <= 256 && pc <= 16;
+          for (uint32_t k = 1, nx = 3; chain_c && k < H.qc_bits; ++k) {
+            if (!((H.qc[k >> 5] >> (k & 31)) & 1u)) continue;
+            while ((nx & (nx - 1)) == 0) ++nx;  // skip the comb bases (powers of two)
+            cslot[k] = nx++;
           }
+        }
+        const uint32_t kend = S.resid ? 256u : (uint32_t)((kCombH - 1) * kCombW) + (nb - 1) * bw;
+        for (uint32_t k = 1; k <= kend; ++k) {
+          op(OP_SQR);
+          if (k % bw == 0 && k / bw < (uint32_t)kCombH * nb) {  // comb base B^(2^(52r + 26t))
+            const uint32_t m = k / bw;
+            op(OP_STORE_TBL, ((m % nb) << kCombH) | (1u << (m / nb)));
+          }
+          if (k % kCombW == 0 && k / kCombW < (uint32_t)kCombH) op(OP_STORE_Y, k / kCombW - 1);
+          if (k < 256 && cslot[k]) op(OP_STORE_TBL, cslot[k]);
         }
         if (S.resid) {
-          for (uint32_t k = (kCombH - 1) * kCombW; k < 256; ++k) op(OP_SQR);
-          op(OP_STORE_R, 0);
-          op(OP_LOAD_TBL, 1);
-          for (int w = (int)H.qc_bits - 2; w >= 0; --w) {
-            op(OP_SQR);
-            if ((H.qc[w >> 5] >> (w & 31)) & 1u) op(OP_MUL_TBL, 1);
+          op(OP_STORE_R, 0);  // z = B^(2^256)
+          if (chain_c) {
+            bool first = true;
+            if (H.qc[0] & 1u) { op(OP_LOAD_TBL, 1); first = false; }
+            for (uint32_t k = 1; k < 256; ++k) {
+              if (!cslot[k]) continue;
+              op(first ? OP_LOAD_TBL : OP_MUL_TBL, cslot[k]);
+              first = false;
+            }
+            if (first) op(OP_LOAD_ONE);
+          } else {
+            op(OP_LOAD_TBL, 1);
+            for (int w = (int)H.qc_bits - 2; w >= 0; --w) {
+              op(OP_SQR);
+              if ((H.qc[w >> 5] >> (w & 31)) & 1u) op(OP_MUL_TBL, 1);
+            }
           }
-          op(OP_STORE_R, 1);
+          op(OP_STORE_R, 1);  // w = B^c
         }
       }
-      for (uint32_t k = 3; k < (1u << kCombH); ++k) {
-        if ((k & (k - 1)) == 0) continue;
-        op(OP_LOAD_TBL, k & (k - 1));
-        op(OP_MUL_TBL, k & (0u - k));
-        op(OP_STORE_TBL, k);
+      for (uint32_t t = 0; t < nb; ++t) {
+        const uint32_t o = t << kCombH;
+        for (uint32_t k = 3; k < (1u << kCombH); ++k) {
+          if ((k & (k - 1)) == 0) continue;
+          op(OP_LOAD_TBL, o + (k & (k - 1)));
+          op(OP_MUL_TBL, o + (k & (0u - k)));
+          op(OP_STORE_TBL, o + k);
+        }
       }
     }
   }
@@ -281,11 +317,12 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
     bool one = true;
     if (S.has_base) {
       op(OP_EXP, o);
-      if (comb) {
-        op(OP_LOAD_COMB, kCombW - 1);
-        for (int w = kCombW - 2; w >= 0; --w) {
+      if (comb) {  // column w of block t is digit t * bw + w (OP_EXP)
+        op(OP_LOAD_COMB, bw - 1);
+        for (uint32_t t = 1; t < nb; ++t) op(OP_MUL_COMB, t * bw + bw - 1);
+        for (int w = (int)bw - 2; w >= 0; --w) {
           op(OP_SQR);
-          op(OP_MUL_COMB, (uint32_t)w);
+          for (uint32_t t = 0; t < nb; ++t) op(OP_MUL_COMB, t * bw + (uint32_t)w);
         }
       } else {
         op(OP_LOAD_WIN, o);
@@ -343,7 +380,7 @@ static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const
 // later gather launch; ygat: the y_k array a gather launch (S.gather > 0) multiplies together.
 // tail (optional): a second, independent job population (shape tail->S) appended to the LAST
 // sub-launch so its short jobs fill that launch's tail (PowPart in eg_kernels.hpp).
-// jobs per k_pow sub-launch (bounds the per-launch scratch: 32 comb entries per job)
+// jobs per k_pow sub-launch (bounds the per-launch scratch: 32 or 64 comb entries per job)
 constexpr size_t kPowMaxJobs = (size_t)1 << 18;
 
 struct PowTail {
@@ -355,7 +392,7 @@ struct PowTail {
   uint32_t* rout;  // residue pairs (tail->S.resid)
 };
 static size_t pow_scratch_per_group(const PowShape& S) {
-  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? (1u << kCombH) : 16u) * kW * 4 : 4;
+  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? ((S.blocks == 2 ? 2u : 1u) << kCombH) : 16u) * kW * 4 : 4;
 }
 // ct = true: the constant-time instantiation k_pow<F, true> for secret exponents (comb shapes
 // without fixed-base terms only); ctab: the shared comb table of S.shared_comb jobs.
@@ -364,6 +401,10 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
                       const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr,
                       bool ct = false, const uint32_t* ctab = nullptr) {
   if (S.resid && (!S.comb || S.gather || !rout)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
+  if (S.blocks > 1 && (S.blocks != 2 || !S.comb || S.gather || S.shared_comb || ct))
+    return fail(EG_ERR_ARG, "two column blocks need a plain variable-time comb shape");
+  if (tail && tail->S.blocks > 1 && (tail->S.blocks != 2 || !tail->S.comb || tail->S.gather || tail->S.shared_comb))
+    return fail(EG_ERR_ARG, "two column blocks need a plain variable-time comb shape");
   if (S.shared_comb && (!S.comb || S.gather || S.resid || !ctab)) return fail(EG_ERR_ARG, "shared comb table missing");
   if (ct && (!S.has_base || !S.comb || S.gather || S.nfb[0] || S.nfb[1] || tail))
     return fail(EG_ERR_ARG, "constant-time jobs are plain comb shapes without fixed-base terms");

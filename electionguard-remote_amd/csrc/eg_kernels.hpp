@@ -320,6 +320,9 @@ struct PowShape {
                        // rout[2 gid], rout[2 gid + 1]; B^q == 1 iff z == w and B != 0 (k_resid_check)
   uint32_t shared_comb;  // comb jobs whose 32-entry subset table is PowPart::ctab (one table for every
                          // job, e.g. the trustee's g^u): no per-job precompute
+  uint32_t blocks;     // Lim-Lee column blocks v of a plain comb (0/1: one block of 52 columns, one
+                       // 32-entry table; 2: two blocks of 26, tables of B^(2^(52r)) and B^(2^(52r+26)),
+                       // 64 entries).  v = 2 pays when the squaring chain runs to 2^256 anyway (resid)
 };
 
 // Constant-time table read for secret digits (k_pow<F, CT = true>, the trustee's shares):
@@ -446,7 +449,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   Mont<F> M;
   M.load(C);
   uint32_t x[kL];
-  const uint32_t tsize = S.comb ? (1u << kCombH) : 16u;
+  const uint32_t tsize = S.comb ? ((S.blocks == 2 ? 2u : 1u) << kCombH) : 16u;
   const uint32_t gid = gid0 + threadIdx.x / kT;
   const bool live = gid < njobs;  // tail groups recompute job njobs-1 and store nothing
   const uint32_t* J = P.jobs + (size_t)(live ? gid : njobs - 1) * kJobWords;
@@ -516,11 +519,13 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
           break;
         case OP_EXP:
           if (S.comb) {
-            // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each)
+            // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each); with
+            // two column blocks, columns 26..51 index the second table (entry 32 + digit)
             const uint8_t* e = scalars + (size_t)J[1 + arg] * 32;
+            const int hi = S.blocks == 2 ? kCombW / 2 : kCombW;
             wave_sync();
             for (int j = glane(); j < kCombW; j += kT) {
-              uint32_t d = 0;
+              uint32_t d = j >= hi ? (1u << kCombH) : 0u;
 #pragma unroll
               for (int r = 0; r < kCombH; ++r) {
                 const int bit = r * kCombW + j;
