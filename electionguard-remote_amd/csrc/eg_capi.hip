@@ -160,6 +160,7 @@ struct eg_ctx {
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
   std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
+  uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
   // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
   size_t pow_slots = 0;
@@ -238,10 +239,11 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
   };
   const bool comb = S.comb != 0;
   const uint32_t nb = (comb && S.blocks == 2) ? 2u : 1u;  // Lim-Lee column blocks
-  const uint32_t bw = (uint32_t)kCombW / nb;             // columns per block
+  const uint32_t ch = comb_rows(S.rows), cw = comb_width(S.rows);  // rows, row width (bits)
+  const uint32_t bw = cw / nb;                           // columns per block
   if (S.has_base && !(comb && S.shared_comb)) {
     op(OP_LOAD_ONE);
-    for (uint32_t t = 0; t < nb; ++t) op(OP_STORE_TBL, t << kCombH);
+    for (uint32_t t = 0; t < nb; ++t) op(OP_STORE_TBL, t << ch);
     op(OP_LOAD_BASE);
     op(OP_STORE_TBL, 1);
     if (!comb) {
@@ -264,21 +266,23 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
         if (S.resid) {
           uint32_t pc = 0;
           for (uint32_t k = 1; k < H.qc_bits && k < 256; ++k) pc += (H.qc[k >> 5] >> (k & 31)) & 1u;
-          chain_c = H.qc_bits <= 256 && pc <= 16;
+          chain_c = H.qc_bits <= 256 && pc <= std::min(16u, (1u << ch) - ch - 1u);
           for (uint32_t k = 1, nx = 3; chain_c && k < H.qc_bits; ++k) {
             if (!((H.qc[k >> 5] >> (k & 31)) & 1u)) continue;
             while ((nx & (nx - 1)) == 0) ++nx;  // skip the comb bases (powers of two)
             cslot[k] = nx++;
           }
         }
-        const uint32_t kend = S.resid ? 256u : (uint32_t)((kCombH - 1) * kCombW) + (nb - 1) * bw;
+        const uint32_t kend = S.resid ? 256u : (ch - 1) * cw + (nb - 1) * bw;
         for (uint32_t k = 1; k <= kend; ++k) {
           op(OP_SQR);
-          if (k % bw == 0 && k / bw < (uint32_t)kCombH * nb) {  // comb base B^(2^(52r + 26t))
+          if (k % bw == 0 && k / bw < ch * nb) {  // comb base B^(2^(cw r + bw t))
             const uint32_t m = k / bw;
-            op(OP_STORE_TBL, ((m % nb) << kCombH) | (1u << (m / nb)));
+            op(OP_STORE_TBL, ((m % nb) << ch) | (1u << (m / nb)));
           }
-          if (k % kCombW == 0 && k / kCombW < (uint32_t)kCombH) op(OP_STORE_Y, k / kCombW - 1);
+          // gather powers y_r = B^(2^(52r)) for the contest jobs (5-row combs)
+          if (ch == (uint32_t)kCombH && k % kCombW == 0 && k / kCombW < (uint32_t)kCombH)
+            op(OP_STORE_Y, k / kCombW - 1);
           if (k < 256 && cslot[k]) op(OP_STORE_TBL, cslot[k]);
         }
         if (S.resid) {
@@ -303,8 +307,8 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
         }
       }
       for (uint32_t t = 0; t < nb; ++t) {
-        const uint32_t o = t << kCombH;
-        for (uint32_t k = 3; k < (1u << kCombH); ++k) {
+        const uint32_t o = t << ch;
+        for (uint32_t k = 3; k < (1u << ch); ++k) {
           if ((k & (k - 1)) == 0) continue;
           op(OP_LOAD_TBL, o + (k & (k - 1)));
           op(OP_MUL_TBL, o + (k & (0u - k)));
@@ -392,7 +396,7 @@ struct PowTail {
   uint32_t* rout;  // residue pairs (tail->S.resid)
 };
 static size_t pow_scratch_per_group(const PowShape& S) {
-  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? ((S.blocks == 2 ? 2u : 1u) << kCombH) : 16u) * kW * 4 : 4;
+  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? ((S.blocks == 2 ? 2u : 1u) << comb_rows(S.rows)) : 16u) * kW * 4 : 4;
 }
 // ct = true: the constant-time instantiation k_pow<F, true> for secret exponents (comb shapes
 // without fixed-base terms only); ctab: the shared comb table of S.shared_comb jobs.
@@ -401,11 +405,14 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
                       const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr,
                       bool ct = false, const uint32_t* ctab = nullptr) {
   if (S.resid && (!S.comb || S.gather || !rout)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
-  if (S.blocks > 1 && (S.blocks != 2 || !S.comb || S.gather || S.shared_comb || ct))
-    return fail(EG_ERR_ARG, "two column blocks need a plain variable-time comb shape");
+  if (S.blocks > 1 && (S.blocks != 2 || !S.comb || S.gather || S.shared_comb))
+    return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
   if (tail && tail->S.blocks > 1 && (tail->S.blocks != 2 || !tail->S.comb || tail->S.gather || tail->S.shared_comb))
-    return fail(EG_ERR_ARG, "two column blocks need a plain variable-time comb shape");
+    return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
   if (S.shared_comb && (!S.comb || S.gather || S.resid || !ctab)) return fail(EG_ERR_ARG, "shared comb table missing");
+  if ((S.rows && (S.rows != 4 || !S.comb || S.gather || S.shared_comb || S.resid)) ||
+      (tail && tail->S.rows))
+    return fail(EG_ERR_ARG, "4-row combs are plain comb shapes without residue pairs");
   if (ct && (!S.has_base || !S.comb || S.gather || S.nfb[0] || S.nfb[1] || tail))
     return fail(EG_ERR_ARG, "constant-time jobs are plain comb shapes without fixed-base terms");
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
@@ -619,6 +626,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
       if ((c->h.qc[b >> 5] >> (b & 31)) & 1u) { c->h.qc_bits = (uint32_t)b + 1; break; }
   }
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
+  if (const char* cr = getenv("EG_CT_ROWS")) c->ct_rows = (cr[0] == '5') ? 0u : 4u;
   {
     int cus = 0, per_cu = 0;
     const char* ts = getenv("EG_TAIL_SPLIT");

@@ -323,13 +323,21 @@ struct PowShape {
   uint32_t blocks;     // Lim-Lee column blocks v of a plain comb (0/1: one block of 52 columns, one
                        // 32-entry table; 2: two blocks of 26, tables of B^(2^(52r)) and B^(2^(52r+26)),
                        // 64 entries).  v = 2 pays when the squaring chain runs to 2^256 anyway (resid)
+  uint32_t rows;       // Lim-Lee rows h of a plain comb (0: kCombH = 5 rows of 52 bits, 32-entry
+                       // tables; 4: rows of 64 bits, 16-entry tables -- the constant-time trustee
+                       // pair, whose masked scans read every entry of a table)
 };
 
 // Constant-time table read for secret digits (k_pow<F, CT = true>, the trustee's shares):
 // every entry of the table is read and the wanted one kept with a mask, so the addresses a
 // job touches do not depend on the digit d.  Each lane selects its own 20-word block.
 __device__ __forceinline__ void ct_select_to_lds(uint32_t* __restrict__ slot, const uint32_t* __restrict__ tbl,
-                                                 int nent, uint32_t d) {
+                                                 uint32_t h, uint32_t d) {
+  // d = block << h | digit: the column block is public (fixed by the column index), so only
+  // its 2^h entries are scanned; the digit selects among them by mask
+  const int nent = 1 << h;
+  tbl += (size_t)(d >> h << h) * kW;
+  d &= (uint32_t)nent - 1u;
   const int o = glane() * kLP;
   uint4 acc[kLP / 4];
 #pragma unroll
@@ -351,9 +359,11 @@ __device__ __forceinline__ void ct_select_to_lds(uint32_t* __restrict__ slot, co
   for (int j = 0; j < kLP / 4; ++j) *reinterpret_cast<uint4*>(slot + o + 4 * j) = acc[j];
 }
 
-// Lim-Lee comb parameters for 256-bit exponents: 5 rows of 52 bits.
+// Lim-Lee comb parameters for 256-bit exponents: 5 rows of 52 bits (PowShape::rows = 4: 4 rows of 64).
 constexpr int kCombH = 5;
 constexpr int kCombW = 52;
+__host__ __device__ constexpr uint32_t comb_rows(uint32_t rows) { return rows ? rows : (uint32_t)kCombH; }
+__host__ __device__ constexpr uint32_t comb_width(uint32_t rows) { return (256u + comb_rows(rows) - 1u) / comb_rows(rows); }
 
 __device__ __forceinline__ uint32_t be_digit(const uint8_t* __restrict__ e, int nbytes, int bit, int wb) {
   uint32_t v = 0;
@@ -449,7 +459,8 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   Mont<F> M;
   M.load(C);
   uint32_t x[kL];
-  const uint32_t tsize = S.comb ? ((S.blocks == 2 ? 2u : 1u) << kCombH) : 16u;
+  const uint32_t ch = comb_rows(S.rows);  // comb rows: table entries per column block = 2^ch
+  const uint32_t tsize = S.comb ? ((S.blocks == 2 ? 2u : 1u) << ch) : 16u;
   const uint32_t gid = gid0 + threadIdx.x / kT;
   const bool live = gid < njobs;  // tail groups recompute job njobs-1 and store nothing
   const uint32_t* J = P.jobs + (size_t)(live ? gid : njobs - 1) * kJobWords;
@@ -498,7 +509,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         case OP_LOAD_WIN: load_elem(x, tbl + (size_t)(scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4) * kW); break;
         case OP_LOAD_COMB:
           if constexpr (CT) {
-            ct_select_to_lds(slot, tbl, 1 << kCombH, dig[arg]);
+            ct_select_to_lds(slot, tbl, ch, dig[arg]);
             wave_sync();
             load_elem(x, slot);
             wave_sync();
@@ -522,14 +533,15 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
             // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each); with
             // two column blocks, columns 26..51 index the second table (entry 32 + digit)
             const uint8_t* e = scalars + (size_t)J[1 + arg] * 32;
-            const int hi = S.blocks == 2 ? kCombW / 2 : kCombW;
+            const int cw = (int)comb_width(S.rows);
+            const int hi = S.blocks == 2 ? cw / 2 : cw;
             wave_sync();
-            for (int j = glane(); j < kCombW; j += kT) {
-              uint32_t d = j >= hi ? (1u << kCombH) : 0u;
+            for (int j = glane(); j < cw; j += kT) {
+              uint32_t d = j >= hi ? (1u << ch) : 0u;
 #pragma unroll
               for (int r = 0; r < kCombH; ++r) {
-                const int bit = r * kCombW + j;
-                if (bit < 256) d |= (((uint32_t)e[31 - (bit >> 3)] >> (bit & 7)) & 1u) << r;
+                const int bit = r * cw + j;
+                if (r < (int)ch && bit < 256) d |= (((uint32_t)e[31 - (bit >> 3)] >> (bit & 7)) & 1u) << r;
               }
               dig[j] = (uint8_t)d;
             }
@@ -543,7 +555,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     // ---- the one Montgomery multiply (or square) ----
     if (ysrc) {
       if constexpr (CT) {
-        if (kind == OP_MUL_COMB) ct_select_to_lds(slot, tbl, 1 << kCombH, dig[arg]);  // secret digit
+        if (kind == OP_MUL_COMB) ct_select_to_lds(slot, tbl, ch, dig[arg]);  // secret digit
         else elem_to_lds(slot, ysrc);
       } else {
         elem_to_lds(slot, ysrc);
