@@ -239,37 +239,96 @@ __global__ void __launch_bounds__(kBlock) k_export(const MontConsts* __restrict_
   slot_to_be(slot, be + (size_t)gid * 512, gid < n);
 }
 
+// Canonical value in [0, p) of a lazy Montgomery-domain value in [0, 2p) held in registers
+// (limbs as mont_mul leaves them): the carry passes of regs_normalize, then x >= p decided by
+// the group's most significant differing limb (each lane compares its own limbs from the top,
+// the highest lane with a difference decides; no difference = equal), and a group-uniform
+// subtraction of p whose borrows ripple between lanes like the carries.
+template <bool F>
+__device__ __forceinline__ void regs_reduce_lazy(const Mont<F>& M, uint32_t (&x)[kL]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) {
+    const uint32_t v = x[j] + c;
+    x[j] = v & kMask;
+    c = v >> kLimbBits;
+  }
+  const bool g0 = glane() == 0;
+  for (int round = 0; round < kT; ++round) {
+    uint32_t cin = from_prev(c);
+    if (g0) cin = 0;
+    if (__ballot(cin != 0) == 0) break;
+    c = 0;
+    if (cin) {
+#pragma unroll
+      for (int j = 0; j < kL; ++j) {
+        const uint32_t v = x[j] + cin;
+        x[j] = v & kMask;
+        cin = v >> kLimbBits;
+      }
+      c = cin;
+    }
+  }
+  bool ne = false, gt = false;
+#pragma unroll
+  for (int j = 0; j < kL; ++j) {  // ascending: the last (most significant) difference wins
+    if (x[j] != M.p[j]) { ne = true; gt = x[j] > M.p[j]; }
+  }
+  const uint32_t sh = gslot() * kT;
+  const uint32_t nem = (uint32_t)(__ballot(ne) >> sh) & ((1u << kT) - 1u);
+  const uint32_t gtm = (uint32_t)(__ballot(gt) >> sh) & ((1u << kT) - 1u);
+  const bool ge = nem == 0 || ((gtm >> (31 - __builtin_clz(nem))) & 1u);
+  if (__ballot(ge) == 0) return;  // no group of the wave needs the subtraction
+  uint32_t b = 0;
+  if (ge) {
+#pragma unroll
+    for (int j = 0; j < kL; ++j) {
+      const uint32_t v = x[j] - M.p[j] - b;
+      x[j] = v & kMask;
+      b = v >> 31;  // limbs < 2^29: a borrow leaves the top bit set
+    }
+  }
+  for (int round = 0; round < kT; ++round) {
+    uint32_t bin = from_prev(b);  // borrow out of the lane below (none out of the top: x >= p)
+    if (g0) bin = 0;
+    if (__ballot(bin != 0) == 0) break;
+    b = 0;
+    if (bin) {
+#pragma unroll
+      for (int j = 0; j < kL; ++j) {
+        const uint32_t v = x[j] - bin;
+        x[j] = v & kMask;
+        bin = v >> 31;
+      }
+      b = bin;
+    }
+  }
+}
+
 // Residue (subgroup) test of n bases from their k_pow residue pairs (PowShape::resid):
 //   pair i = (z, w) = (B^(2^256), B^c) in Montgomery form;  B^q == 1  <=>  z == w and B != 0
-// (B^(2^256) = B^q * B^c, and B is invertible unless B == 0, where z = w = 0).
-// flags[i * fstride] &= verdict — the per-element range flag of the verifier (k_import).
-// Cost: 2 MM (leaving the Montgomery domain) + two lane-parallel normalisations per base.
+// (B^(2^256) = B^q * B^c, and B is invertible unless B == 0, where z = w = 0).  zR == wR (mod p)
+// iff z == w, and zR == 0 iff z == 0, so the test runs on the Montgomery forms reduced to
+// [0, p) with no multiply.  flags[i * fstride] &= verdict — the per-element range flag of the
+// verifier (k_import).  Cost: two lane-parallel reductions per base (no MM).
 template <bool F>
 __global__ void __launch_bounds__(kBlock) k_resid_check(const MontConsts* __restrict__ C,
                                                         const uint32_t* __restrict__ pairs, uint32_t n,
                                                         uint8_t* __restrict__ flags, uint32_t fstride) {
   const uint32_t gid = group_id();
   const uint32_t e = gid < n ? gid : n - 1;
-  uint32_t* slot = group_slot();
   Mont<F> M;
   M.load(C);
   uint32_t z[kL], x[kL];
+  load_elem(z, pairs + (size_t)e * 2 * kW);
+  load_elem(x, pairs + ((size_t)e * 2 + 1) * kW);
+  regs_reduce_lazy(M, z);
+  regs_reduce_lazy(M, x);
   bool eq = true, nz = false;
-#pragma unroll 1
-  for (int h = 0; h < 2; ++h) {
-    load_elem(x, pairs + ((size_t)e * 2 + h) * kW);
-    elem_to_lds(slot, C->unit);
-    wave_sync();
-    M.mul(x, slot);  // value in [0, p]
-    wave_sync();
-    regs_normalize(M, x);  // canonical limbs, p -> 0
-    if (h == 0) {
 #pragma unroll
-      for (int j = 0; j < kL; ++j) { z[j] = x[j]; nz |= z[j] != 0; }
-    } else {
-#pragma unroll
-      for (int j = 0; j < kL; ++j) eq &= z[j] == x[j];
-    }
+  for (int j = 0; j < kL; ++j) {
+    eq &= z[j] == x[j];
+    nz |= z[j] != 0;
   }
   const uint64_t neq = __ballot(!eq), nzb = __ballot(nz);
   const uint64_t gmask = (uint64_t)((1u << kT) - 1u) << (gslot() * kT);
