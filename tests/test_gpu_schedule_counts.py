@@ -1,0 +1,65 @@
+"""GPU: the Montgomery-multiply counts of the op programs k_pow runs, pinned per unit of
+work (eg_ctx_profile_end counts them from the programs of the timed launches):
+
+* verifier, 4 x (5+1) manifest: per selection the alpha job's 465 + 2 W and the beta job's
+  465 + 3 W (256-step squaring chain, 5 for w = B^189, 2 x 26 two-block subset products,
+  2 x 76 comb, then 2 or 3 fixed-base terms of W = ceil(256 / window bits) table windows
+  each), per contest 148 + W (A) and 148 + 2 W (B) gathered combs: 25,088 MM per ballot at
+  the bench's 22-bit tables (W = 12), 27,728 at the default 8-bit ones (W = 32);
+* trustee share: 434 MM for the constant-time 4-row comb pair (A^s, A^u) + 102 for g^u
+  from g's shared comb table.
+The verdicts of the profiled batches are checked too (the counts are of real work)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+
+def verify_mm_per_ballot(window_bits: int) -> int:
+    W = -(-256 // window_bits)
+    return 24 * ((465 + 2 * W) + (465 + 3 * W)) + 4 * ((148 + W) + (148 + 2 * W))
+
+
+TRUSTEE_MM_PER_TEXT = (224 + 2 * 11 + 2 * (31 + 63)) + (1 + 51 * 2 - 1)
+
+
+def test_verifier_mm_per_ballot(group):
+    from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
+    from electionguard.keyceremony import key_ceremony
+    assert verify_mm_per_ballot(22) == 25088 and verify_mm_per_ballot(8) == 27728
+    man = Manifest(4, 5, 1)
+    _, K = key_ceremony(group, 3, 3, seed=5)
+    key = ElectionKey(group, K)
+    rng = np.random.default_rng(9)
+    nb = 300
+    eb = batch_encryption(group, key, 77, man, random_votes(rng, man, nb),
+                          random_scalars(rng, (nb, man.nsel, 4), group.q), random_scalars(rng, (nb, man.n_contests), group.q))
+    V = Verifier(group, key, 77, man)
+    V.verify(eb.slice(0, 1))  # warm-up: key registration and job tables outside the window
+    group.profile_begin()
+    ok_s, ok_c, _ = V.verify(eb)
+    kp = group.profile_end()
+    assert ok_s.all() and ok_c.all()
+    assert kp.mont_ops == nb * verify_mm_per_ballot(key.window_bits), kp
+
+
+def test_trustee_mm_per_text(group):
+    from electionguard.ballot import random_scalars
+    from electionguard.decrypt import partial_decrypt_batch
+    assert TRUSTEE_MM_PER_TEXT == 536
+    rng = np.random.default_rng(4)
+    n = 700
+    R = random_scalars(rng, (n,), group.q)
+    pads = group.gPowP_batch(R)
+    texts = np.ascontiguousarray(np.stack([pads, pads], axis=1))
+    nonces = random_scalars(rng, (n,), group.q)
+    s = 0x1234567890ABCDEF
+    partial_decrypt_batch(group, s, 99, texts[:2], nonces[:2])  # warm-up: g's shared comb table
+    group.profile_begin()
+    M, _ = partial_decrypt_batch(group, s, 99, texts, nonces)
+    kp = group.profile_end()
+    assert kp.mont_ops == n * TRUSTEE_MM_PER_TEXT, kp
+    for i in (0, n // 2, n - 1):
+        P = int.from_bytes(pads[i].tobytes(), "big")
+        assert int.from_bytes(M[i].tobytes(), "big") == pow(P, s, group.p), i
