@@ -453,6 +453,7 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
       HIPCHK(hipEventCreate(&pr.a));
       HIPCHK(hipEventCreate(&pr.b));
       HIPCHK(hipMalloc(&pr.d_clk, (size_t)grid.x * 2 * sizeof(uint64_t)));
+      HIPCHK(hipMemsetAsync(pr.d_clk, 0, (size_t)grid.x * 2 * sizeof(uint64_t), c->stream));
       pr.nblocks = grid.x;
       HIPCHK(hipEventRecord(pr.a, c->stream));
     }
@@ -901,10 +902,17 @@ extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr
     if (r.d_clk) {
       std::vector<uint64_t> h((size_t)r.nblocks * 2);
       HIPCHK(hipMemcpy(h.data(), r.d_clk, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      uint32_t unset = 0;
       for (uint32_t b = 0; b < r.nblocks; ++b) {
+        if (h[2 * b + 1] == 0) {  // workgroup record not written (must not happen)
+          ++unset;
+          continue;
+        }
         cyc += (double)h[2 * b];
         wall += (double)h[2 * b + 1];
       }
+      if (unset && getenv("EG_DEBUG_CLK"))
+        fprintf(stderr, "eg_ctx_profile_end: %u of %u workgroup clock records unset\n", unset, r.nblocks);
       hipFree(r.d_clk);
     }
     hipEventDestroy(r.a);
