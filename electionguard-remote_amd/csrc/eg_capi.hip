@@ -394,6 +394,7 @@ struct PowTail {
   uint32_t* yout;
   const uint32_t* ygat;
   uint32_t* rout;  // residue pairs (tail->S.resid)
+  const uint32_t* ctab;  // shared comb table (tail->S.shared_comb)
 };
 static size_t pow_scratch_per_group(const PowShape& S) {
   return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? ((S.blocks == 2 ? 2u : 1u) << comb_rows(S.rows)) : 16u) * kW * 4 : 4;
@@ -413,8 +414,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   if ((S.rows && (S.rows != 4 || !S.comb || S.gather || S.shared_comb || S.resid)) ||
       (tail && tail->S.rows))
     return fail(EG_ERR_ARG, "4-row combs are plain comb shapes without residue pairs");
-  if (ct && (!S.has_base || !S.comb || S.gather || S.nfb[0] || S.nfb[1] || tail))
+  auto ct_shape = [](const PowShape& X) { return X.has_base && X.comb && !X.gather && !X.nfb[0] && !X.nfb[1]; };
+  if (ct && (!ct_shape(S) || (tail && !ct_shape(tail->S))))
     return fail(EG_ERR_ARG, "constant-time jobs are plain comb shapes without fixed-base terms");
+  if (tail && tail->S.shared_comb && (!tail->S.comb || tail->S.gather || tail->S.resid || !tail->ctab))
+    return fail(EG_ERR_ARG, "shared comb table missing");
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
   if (tail && tail->S.gather && (!tail->S.comb || !tail->ygat))
     return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
@@ -444,7 +448,7 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     PowPart P1{};
     if (nt) {
       P1 = PowPart{tail->S, sched_tail, tail->jobs, (uint32_t)nt, grid_for(nt),
-                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, tail->rout, nullptr};
+                   scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, tail->rout, tail->ctab};
     }
     ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
