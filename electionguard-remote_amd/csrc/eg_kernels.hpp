@@ -375,7 +375,7 @@ struct PowShape {
                        // aggregates A = prod alpha, B = prod beta): y_k = prod of their y_k (ygat,
                        // job J[2] onwards) instead of 208 squarings; 0 = none
   uint32_t resid;      // comb jobs (not gather): also write the residue-test pair of the base B,
-                       // z = B^(2^256) (48 squarings past y_4) and w = B^c, c = 2^256 - q, to
+                       // z = B^(2^256) (the squaring chain run to the end) and w = B^c, c = 2^256 - q, to
                        // rout[2 gid], rout[2 gid + 1]; B^q == 1 iff z == w and B != 0 (k_resid_check)
   uint32_t shared_comb;  // comb jobs whose 32-entry subset table is PowPart::ctab (one table for every
                          // job, e.g. the trustee's g^u): no per-job precompute
