@@ -1,4 +1,4 @@
-"""CPU: the N>1 path with world_size 2 over gloo — ballot shards, verdict all-reduce and
+"""CPU: the N>1 path with world_size 2 and 4 over gloo — ballot shards, verdict all-reduce and
 the all-gather + mod-p fold of partial tallies (the fold is the oracle's product here;
 on the GPU it is GroupContext.prodP_groups)."""
 import os
@@ -52,10 +52,11 @@ def _worker(rank, world, port, data, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_tally_fold_equals_global_tally():
+@pytest.mark.parametrize("world", [2, 4])
+def test_n_rank_tally_fold_equals_global_tally(world):
     G = O.production_group()
     rng = random.Random(5)
-    nb, n_real = 7, 3  # ragged shards 4 + 3
+    nb, n_real = 7, 3  # ragged shards: 4 + 3 (2 ranks), 2 + 2 + 2 + 1 (4 ranks)
     cts = np.zeros((nb, n_real, 2, 512), np.uint8)
     for i in range(nb):
         for s in range(n_real):
@@ -64,7 +65,7 @@ def test_two_rank_tally_fold_equals_global_tally():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, (cts, n_real), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, (cts, n_real), q)) for r in range(world)]
     for p in procs:
         p.start()
     ok, bad, tally = q.get(timeout=120)
