@@ -201,3 +201,35 @@ def test_share_backups_gpu_ceremony_and_trustee(group):
     t1 = DecryptingTrustee(group, gk[1], comm)
     with pytest.raises(ValueError):
         t1.compensatedDecrypt(group, gk[3].gid, np.zeros((1, 2, 512), np.uint8), 5)
+
+
+def test_trustee_batch_past_one_sublaunch(group):
+    """More texts than one k_pow sub-launch holds (2^18 jobs): the constant-time pair jobs
+    split into two sub-launches and the g^u jobs ride as the last one's second part. Every
+    share proof verifies on the mediator path, and M is checked with CPython pow around the
+    sub-launch boundary."""
+    import ctypes
+    from electionguard.ballot import random_scalars
+    from electionguard.core import native
+    from electionguard.core.group import p_bytes, q_bytes
+    from electionguard.decrypt import partial_decrypt_batch
+    from electionguard.keyceremony import key_ceremony
+    gk, K = key_ceremony(group, 2, 2, seed=91)
+    rng = np.random.default_rng(91)
+    n = (1 << 18) + 1000
+    R = random_scalars(rng, (n,), group.q)
+    pads = group.gPowP_batch(R)
+    T = np.ascontiguousarray(np.stack([pads, pads], axis=1))
+    qbar = 0x5EED
+    s = gk[0].secret
+    M, pr = partial_decrypt_batch(group, s, qbar, T, random_scalars(rng, (n,), group.q))
+    for i in (0, (1 << 18) - 1, 1 << 18, n - 1):
+        P = int.from_bytes(pads[i].tobytes(), "big")
+        assert int.from_bytes(M[i].tobytes(), "big") == pow(P, s, group.p), i
+    ok = np.zeros(n, np.uint8)
+    Ki = np.ascontiguousarray(np.tile(np.frombuffer(p_bytes(gk[0].public_key), np.uint8), (n, 1)))
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    native.check(group._lib, "eg_verify_shares",
+                 group._lib.eg_verify_shares(group.handle, native.buf(q_bytes(qbar)), ptr(Ki), ptr(T), ptr(M),
+                                             ptr(pr), n, ptr(ok)))
+    assert ok.all()
