@@ -66,6 +66,8 @@ struct Mont {
   __device__ __forceinline__ void mul(uint32_t (&x)[kL], const uint32_t* y) const {
     mont_mul_impl<F, false>(x, y, p, n0, mask);
   }
+  // x <- x * R^-1 (leave the Montgomery domain; no multiplier operand)
+  __device__ __forceinline__ void redc(uint32_t (&x)[kL]) const { mont_redc_impl<F>(x, p, n0, mask); }
   // x <- x^2 (the slot must hold x); symmetric-half schedule (EG_SQR) or plain CIOS
   __device__ __forceinline__ void sqr(uint32_t (&x)[kL], const uint32_t* y) const {
 #if EG_SQR
@@ -229,10 +231,7 @@ __global__ void __launch_bounds__(kBlock) k_export(const MontConsts* __restrict_
   M.load(C);
   uint32_t x[kL];
   load_elem(x, in + (size_t)e * kW);
-  elem_to_lds(slot, C->unit);
-  wave_sync();
-  M.mul(x, slot);  // leave the Montgomery domain: value in [0, p]
-  wave_sync();
+  M.redc(x);  // leave the Montgomery domain: value in [0, p]
   regs_normalize(M, x);
   regs_to_lds(slot, x);
   wave_sync();
