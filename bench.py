@@ -1,12 +1,15 @@
 """Benchmark: ballots verified+tallied per second on the EG 1.0 4096-bit group.
 
-Workload (BASELINE.json configs[1]): per GPU, 10k synthetic ballots of 4 contests x 5
-selections (+1 placeholder each, 24 encrypted selections per ballot), batch-encrypted on
-the GPU in setup (untimed, reported separately), then ONE step = verify every ballot's
-disjunctive and contest proofs + homomorphic tally of all ballots, with the encrypted
-ballots already resident in HBM.  For N GPUs (torch.distributed.run, one rank per GPU)
-every rank verifies its own 10k-ballot shard (weak scaling) and the per-rank partial
-tallies are all-gathered over RCCL and folded mod p on rank 0.
+Workload: synthetic ballots of 4 contests x 5 selections (+1 placeholder each, 24 encrypted
+selections per ballot), batch-encrypted on the GPU in setup (untimed, reported separately),
+then ONE step = verify every ballot's disjunctive and contest proofs + homomorphic tally of all
+ballots, with the encrypted ballots already resident in HBM.
+  * N = 1: BASELINE.json configs[1], 10k ballots on one GPU.
+  * N > 1 (torch.distributed.run or self-launched, one rank per GPU): configs[2], 1M ballots
+    over the node, 1_000_000 // N contiguous ballots per rank (a fixed total: strong scaling);
+    the per-rank partial tallies are all-gathered over RCCL and folded mod p on rank 0.
+  * --manifest large: the configs[4] manifest (20 contests x 5 selections, 120 encrypted
+    selections per ballot), same ballot counts unless --ballots is given.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the roofline definition.
 """
@@ -35,16 +38,34 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--ballots", type=int, default=10000, help="ballots per GPU")
-    ap.add_argument("--contests", type=int, default=4)
+    ap.add_argument("--ballots", type=int, default=0,
+                    help="ballots per GPU (0 = the config's: 10k at N = 1 (configs[1]), 1M // N for N > 1 (configs[2]))")
+    ap.add_argument("--manifest", choices=("small", "large"), default="small",
+                    help="small = 4 contests x 5 selections (configs[1-2]); large = 20 x 5 (configs[4])")
+    ap.add_argument("--contests", type=int, default=0, help="override the manifest's contests")
     ap.add_argument("--selections", type=int, default=5)
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="seconds a collective (and the rank launcher) may wait before failing")
     ap.add_argument("--fb-window", type=int, default=22, help="fixed-base radix window bits for g and K")
     ap.add_argument("--cpu-sample", type=int, default=1, help="run the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the affinity count)")
     ap.add_argument("--modexp-n", type=int, default=1 << 20,
                     help="modexp microbenchmark batch per GPU (SURVEY 8(d): 2^20; 0 = skip)")
-    return ap.parse_args()
+    ap.add_argument("--ct-encrypt", type=int, default=1,
+                    help="also time the constant-time encryption mode (eg_ctx_set_ct_encrypt; 0 = skip)")
+    a = ap.parse_args()
+    if not a.contests:
+        a.contests = 20 if a.manifest == "large" else 4
+    if not a.ballots:
+        a.ballots = default_ballots(a.gpus)
+    return a
+
+
+def default_ballots(gpus: int) -> int:
+    """Ballots per GPU of the BASELINE config bench.py measures at N GPUs: configs[1] (10k on one
+    GPU) at N = 1, configs[2] (1M ballots over the node) at N > 1."""
+    return 10_000 if gpus <= 1 else 1_000_000 // gpus
 
 
 def main():
@@ -53,8 +74,9 @@ def main():
     lw = launched_world()
     if lw is None and a.gpus > 1:
         # no launcher: start one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*) before
-        # anything touches HIP; rank 0 prints the JSON line, this parent returns the worst status
-        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus))
+        # anything touches HIP; rank 0 prints the JSON line; the first rank to fail ends the run
+        # (the others are killed) and its status is this process's
+        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus, timeout=a.dist_timeout * 4))
     if lw is not None and lw != a.gpus:
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={lw} ranks")
     world = lw or 1
@@ -68,13 +90,16 @@ def main():
     if backend == "gloo":
         local = 0
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
+        tmo = datetime.timedelta(seconds=a.dist_timeout)  # a dead peer fails the collective, not hangs it
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     else:
         torch.cuda.set_device(local)
 
@@ -113,6 +138,13 @@ def main():
     d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     enc_dev = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev)
+    enc_dev_ct = None
+    if a.ct_encrypt:  # constant-time mode (masked table scans, no secret-indexed address): same bytes
+        group.ct_encrypt = True
+        try:
+            enc_dev_ct = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2)
+        finally:
+            group.ct_encrypt = False
     # modexp/sec/GPU microbenchmark, run before the verify step so the verify
     # launches stay the last k_pow dispatches of the process (tools/prof_summary.py)
     modexp = modexp_ubench(group, a.modexp_n, dev, rank) if a.modexp_n > 0 else None
@@ -156,6 +188,10 @@ def main():
     build_id = hashlib.md5(Path(native.lib_path()).read_bytes()).hexdigest()[:12]
     total_ballots = nb * world * a.steps
     cfg_name = config_name(a.contests, a.selections, nb, world)
+    clock = kp.clock_ghz if kp.clock_ghz and 1.0 <= kp.clock_ghz <= 2.6 else None
+    clock_note = (f"median of {kp.clock_records} workgroup records, {kp.clock_dropped} dropped" if clock else
+                  f"null: median {kp.clock_ghz:.3f} GHz outside [1.0, 2.6] ({kp.clock_records} records used, "
+                  f"{kp.clock_dropped} dropped as unset, wrapped or out of range)")
     coll = "RCCL" if (dist is None or backend == "nccl") else backend
     value = total_ballots / el
     # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
@@ -171,14 +207,14 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(el / a.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 and nb * world == 1_000_000 else "weak",
         "vs_baseline": None,
         "dtype": f"u32xu32->u64 (radix-2^{radix} limbs)",
         "data": "synthetic (seeded random one-hot ballots, GPU-encrypted with random nonces)",
         "config": {
-            "workload": f"{cfg_name}: verify + homomorphic tally of {nb} ballots per GPU, "
-                        f"{a.contests} contests x {a.selections} selections (+1 placeholder), "
-                        "EG 1.0 4096-bit production group",
+            "workload": f"{cfg_name}: verify + homomorphic tally of {nb} ballots per GPU "
+                        f"({nb * world} in total), {a.contests} contests x {a.selections} selections "
+                        "(+1 placeholder), EG 1.0 4096-bit production group",
             "ballots_per_gpu": nb,
             "selections_per_ballot": man.nsel,
             "fb_window_bits": a.fb_window,
@@ -195,9 +231,9 @@ def main():
             "frac_of_measured_issue_peak": round(achieved / ISSUE_TMAC, 4) if achieved else None,
             # the shader clock the timed k_pow launches ran at (boxes run 2.1-2.3 GHz under this
             # load) and `frac` re-based on the peak at that clock (peak is quoted at 2.4 GHz)
-            "clock_ghz": round(kp.clock_ghz, 3) if kp.clock_ghz else None,
-            "frac_at_measured_clock": round(achieved / (PEAK_TMAC * kp.clock_ghz / 2.4), 4)
-            if achieved and kp.clock_ghz else None,
+            "clock_ghz": round(clock, 3) if clock else None,
+            "clock_source": f"in-kernel s_memtime / s_memrealtime x 100 MHz, {clock_note}",
+            "frac_at_measured_clock": round(achieved / (PEAK_TMAC * clock / 2.4), 4) if achieved and clock else None,
             "traffic": None,
             "kernel_ms_per_launch": round(kms / max(klaunch, 1), 3),
             "launches": klaunch,
@@ -205,13 +241,17 @@ def main():
             "squaring_frac": round(kp.squarings / kmm, 4) if kmm else None,
         },
         "mont_ops_per_ballot": round(mm_per_ballot, 1) if mm_per_ballot else None,
-        # per ballot: 4 variable-base + 5 fixed-base exponentiations per selection (a0 b0 a1 b1),
-        # 2 + 3 per contest (a, b of the constant proof): 104 + 132 at 4 x (5+1)
-        "modexp_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
-        "modexp_var_base_per_s_per_gpu": round((4 * man.nsel + 2 * man.n_contests) * value / world, 1),
-        "modexp_fixed_base_per_s_per_gpu": round((5 * man.nsel + 3 * man.n_contests) * value / world, 1),
+        # BASELINE's second metric, MEASURED by the modexp microbenchmark (2^20 independent
+        # 256-bit exponentiations per GPU, operands in HBM): variable base and fixed base g
+        "modexp_per_s_per_gpu": {"var_base": modexp.get("var_base_per_s"), "fixed_base_g": modexp.get("fixed_base_g_per_s")}
+        if modexp else None,
+        # a derived count, not a measurement: the verify step's work expressed in 256-bit
+        # exponentiations (4 variable-base + 5 fixed-base per selection, 2 + 3 per contest; comb-
+        # shared pairs and fused fixed-base terms counted as whole exponentiations)
+        "modexp_equivalents_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
         "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
         "encrypt_ballots_per_s_per_gpu_device_resident": enc_dev,
+        "encrypt_ballots_per_s_per_gpu_device_resident_constant_time": enc_dev_ct,
         "modexp_ubench": modexp,
         "build": build_id,
     }
@@ -238,7 +278,8 @@ def main():
 
 def config_name(contests: int, selections: int, nb: int, world: int) -> str:
     """BASELINE.json config this run measures: configs[1] = 10k ballots of 4 x 5 on ONE GPU;
-    configs[2] = 1M ballots of 4 x 5 over the node; configs[4] = the 100-selection manifest."""
+    configs[2] = 1M ballots of 4 x 5 over the node; configs[4] = 1M ballots of the 100-selection
+    manifest (20 x 5) at 1/2/4/8 GPUs."""
     total = nb * world
     gpus = f"{world} GPU{'s' if world > 1 else ''}"
     if (contests, selections) == (4, 5):
@@ -248,6 +289,8 @@ def config_name(contests: int, selections: int, nb: int, world: int) -> str:
             return "configs[1]"
         return f"configs[1] shape (4x5), {nb} ballots per GPU x {gpus}"
     if (contests, selections) == (20, 5):
+        if total == 1_000_000:
+            return f"configs[4] (1M ballots of 20x5 over {gpus})"
         return f"configs[4] shape (20x5), {nb} ballots per GPU x {gpus}"
     return f"custom manifest {contests}x{selections}, {nb} ballots per GPU x {gpus}"
 

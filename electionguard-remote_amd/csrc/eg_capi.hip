@@ -17,8 +17,12 @@
 #include <cstring>
 #include <deque>
 #include <array>
+#include <chrono>
+#include <condition_variable>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -111,12 +115,14 @@ struct DevBuf {
 };
 
 struct ProfRec {
-  hipEvent_t a, b;
-  double mm;   // Montgomery operations (multiplies + squarings)
-  double sqr;  // of which squarings (symmetric-half schedule)
-  uint64_t* d_clk = nullptr;  // per workgroup (shader cycles, wall ticks) of the launch (k_pow clk)
-  uint32_t nblocks = 0;
+  hipEvent_t a = nullptr, b = nullptr;
+  double mm = 0;   // Montgomery operations (multiplies + squarings)
+  double sqr = 0;  // of which squarings (symmetric-half schedule)
 };
+// Per-workgroup clock records of the profiled k_pow launches: one device buffer per profile
+// window (allocated by eg_ctx_profile_begin, so nothing is allocated inside the timed launches),
+// (s_memtime ticks, s_memrealtime ticks) per workgroup, launches appended in order.
+constexpr size_t kClockRecs = (size_t)1 << 20;
 
 // Montgomery operations of one k_pow job, split into squarings and multiplies: counted from
 // the job's op program itself (pow_schedule), so the profile's MM totals are the kernel's work.
@@ -137,7 +143,7 @@ struct eg_fixed_base {
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_RC, W_CRF, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_RC, W_CRF, W_CAST, W_NSLOT
 };
 
 struct eg_ctx {
@@ -156,10 +162,16 @@ struct eg_ctx {
   DevBuf ws[W_NSLOT];
   bool timing = false;
   std::vector<ProfRec> prof;
+  uint64_t* d_clk = nullptr;  // kClockRecs x 2 clock records of the open profile window
+  size_t clk_used = 0;        // records handed out in this window
+  uint32_t clk_used_last = 0, clk_dropped_last = 0;  // of the last closed window (eg_ctx_profile_clock)
   uint8_t K_be[512];
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
   std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
+  uint32_t ct_encrypt = 0;              // encryption on k_pow<F, true> with small CT tables (eg_ctx_set_ct_encrypt)
+  eg_fixed_base *g_ct = nullptr, *K_ct = nullptr;  // their kCtEncWindow-bit tables of g and K
+  uint8_t K_ct_be[512];
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
   // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
@@ -168,11 +180,13 @@ struct eg_ctx {
   // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
   // most recently used first
   std::vector<std::pair<std::array<uint8_t, 512>, eg_fixed_base*>> share_keys;
+  // per-element calls from many threads gathered into batches (eg_capi_coalesce.inc)
+  struct Coalescer* co = nullptr;
+  std::mutex co_mu;  // guards the lazy creation of co
   // host-pointer verify: uploads of chunk k+1 on their own stream overlap chunk k's kernels
   hipStream_t copy = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
 };
-static std::vector<ProfRec>& prof_of(eg_ctx* c) { return c->prof; }
 
 static int ws_get(eg_ctx* c, Slot s, size_t bytes, void** out) {
   DevBuf& b = c->ws[s];
@@ -340,7 +354,8 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
     for (uint32_t t = 0; t < S.nfb[o]; ++t) {
       const uint32_t tab = S.tab[o][t] ? 1u : 0u;
       const FbTab& T = tab ? f1 : f0;
-      for (uint32_t kf = 0; kf < T.nwin; ++kf) {
+      const uint32_t nw = S.fb_small[o][t] ? 1u : T.nwin;  // a scalar < 2^wbits needs window 0 only
+      for (uint32_t kf = 0; kf < nw; ++kf) {
         op(one ? OP_LOAD_FB : OP_MUL_FB, fb_arg(o, t, tab, kf));
         one = false;
       }
@@ -386,6 +401,11 @@ static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const
 // sub-launch so its short jobs fill that launch's tail (PowPart in eg_kernels.hpp).
 // jobs per k_pow sub-launch (bounds the per-launch scratch: 32 or 64 comb entries per job)
 constexpr size_t kPowMaxJobs = (size_t)1 << 18;
+// widest radix table a constant-time fixed-base term scans (2^w entries per multiply)
+constexpr uint32_t kCtMaxWindow = 8;
+// radix width of the constant-time encryption tables of g and K (eg_ctx_set_ct_encrypt):
+// 43 windows of 64 entries, 1.76 MB per base
+constexpr int kCtEncWindow = 6;
 
 struct PowTail {
   PowShape S;
@@ -401,10 +421,15 @@ static size_t pow_scratch_per_group(const PowShape& S) {
 }
 // ct = true: the constant-time instantiation k_pow<F, true> for secret exponents (comb shapes
 // without fixed-base terms only); ctab: the shared comb table of S.shared_comb jobs.
+// scratch (optional): the per-job table space of a batch of at most one workgroup and no tail
+// (the caller keeps the tables, e.g. g's shared comb table; it must hold kGroupsPerBlock jobs'
+// tables, since idle groups recompute the last job); default the W_SCR workspace.
 static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
                       const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1, uint32_t* yout = nullptr,
                       const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr,
-                      bool ct = false, const uint32_t* ctab = nullptr) {
+                      bool ct = false, const uint32_t* ctab = nullptr, uint32_t* scratch = nullptr) {
+  if (scratch && (tail || njobs > kPowMaxJobs || njobs > kGroupsPerBlock))
+    return fail(EG_ERR_ARG, "an explicit k_pow scratch takes one workgroup of jobs and no tail");
   if (S.resid && (!S.comb || S.gather || !rout)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
   if (S.blocks > 1 && (S.blocks != 2 || !S.comb || S.gather || S.shared_comb))
     return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
@@ -414,9 +439,14 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   if ((S.rows && (S.rows != 4 || !S.comb || S.gather || S.shared_comb || S.resid)) ||
       (tail && tail->S.rows))
     return fail(EG_ERR_ARG, "4-row combs are plain comb shapes without residue pairs");
-  auto ct_shape = [](const PowShape& X) { return X.has_base && X.comb && !X.gather && !X.nfb[0] && !X.nfb[1]; };
+  // constant-time shapes: a comb (masked scans of its tables) without fixed-base terms, or
+  // fixed-base terms alone from small-window tables (masked scans of 2^w-entry window columns)
+  auto ct_shape = [&](const PowShape& X) {
+    if (X.has_base) return X.comb && !X.gather && !X.nfb[0] && !X.nfb[1];
+    return f0.wbits <= kCtMaxWindow && f1.wbits <= kCtMaxWindow;
+  };
   if (ct && (!ct_shape(S) || (tail && !ct_shape(tail->S))))
-    return fail(EG_ERR_ARG, "constant-time jobs are plain comb shapes without fixed-base terms");
+    return fail(EG_ERR_ARG, "constant-time jobs are plain combs or small-window fixed-base terms");
   if (tail && tail->S.shared_comb && (!tail->S.comb || tail->S.gather || tail->S.resid || !tail->ctab))
     return fail(EG_ERR_ARG, "shared comb table missing");
   if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
@@ -440,9 +470,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     const size_t nj = std::min(max_jobs, njobs - off);
     const bool last = off + nj >= njobs;
     const size_t nt = (last && tail) ? tail->njobs : 0;
-    uint32_t* scr = nullptr;
-    int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
-    if (rc) return rc;
+    uint32_t* scr = scratch;
+    if (!scr) {
+      const int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
+      if (rc) return rc;
+    }
     PowPart P0{S, sched, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
                yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat, rout ? rout + off * 2 * kW : nullptr, ctab};
     PowPart P1{};
@@ -450,18 +482,23 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
       P1 = PowPart{tail->S, sched_tail, tail->jobs, (uint32_t)nt, grid_for(nt),
                    scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, tail->rout, tail->ctab};
     }
-    ProfRec pr{nullptr, nullptr, (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
-               mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt};
     const dim3 grid(P0.nblocks + P1.nblocks);
+    ProfRec* pr = nullptr;
+    uint64_t* clk = nullptr;
     if (c->timing) {
-      HIPCHK(hipEventCreate(&pr.a));
-      HIPCHK(hipEventCreate(&pr.b));
-      HIPCHK(hipMalloc(&pr.d_clk, (size_t)grid.x * 2 * sizeof(uint64_t)));
-      HIPCHK(hipMemsetAsync(pr.d_clk, 0, (size_t)grid.x * 2 * sizeof(uint64_t), c->stream));
-      pr.nblocks = grid.x;
-      HIPCHK(hipEventRecord(pr.a, c->stream));
+      // the record joins the window before anything can fail, so profile_end / destroy free its events
+      c->prof.push_back(ProfRec{nullptr, nullptr,
+                                (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
+                                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt});
+      pr = &c->prof.back();
+      HIPCHK(hipEventCreate(&pr->a));
+      HIPCHK(hipEventCreate(&pr->b));
+      if (c->d_clk && c->clk_used + grid.x <= kClockRecs) {  // else this launch goes unclocked
+        clk = c->d_clk + 2 * c->clk_used;
+        c->clk_used += grid.x;
+      }
+      HIPCHK(hipEventRecord(pr->a, c->stream));
     }
-    uint64_t* clk = pr.d_clk;
     if (c->h.friendly) {
       if (ct) hipLaunchKernelGGL((k_pow<true, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
       else hipLaunchKernelGGL((k_pow<true, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
@@ -470,10 +507,7 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
       else hipLaunchKernelGGL((k_pow<false, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
     }
     HIPCHK(hipGetLastError());
-    if (c->timing) {
-      HIPCHK(hipEventRecord(pr.b, c->stream));
-      prof_of(c).push_back(pr);
-    }
+    if (pr) HIPCHK(hipEventRecord(pr->b, c->stream));
     off += nj;
   } while (off < njobs);
   return EG_OK;
@@ -481,8 +515,9 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
 
 // Product reduction of `groups` groups of `len` device elements (group layout gm,
 // element stride `stride`); result -> d_out[g].  Fully asynchronous.
+// mask (optional, len bytes): element k takes part only if mask[k] != 0 (first pass only).
 static int run_prod(eg_ctx* c, const uint32_t* d_in, GroupMap gm, size_t groups, size_t len, size_t stride,
-                    uint32_t* d_out) {
+                    uint32_t* d_out, const uint8_t* mask = nullptr) {
   if (!groups) return EG_OK;
   if (len == 0) return fail(EG_ERR_ARG, "empty product");
   // Short products (contest aggregates, residue pairs: len = spc) run in one pass.  Long ones
@@ -504,9 +539,10 @@ static int run_prod(eg_ctx* c, const uint32_t* d_in, GroupMap gm, size_t groups,
     uint32_t* dst = (nchunk == 1) ? d_out : ping[pi];
     const size_t njobs = groups * nchunk;
     LAUNCH_F(c, k_prod, dim3(grid_for(njobs)), c->d, src, gm, (uint32_t)groups,
-                       (uint32_t)cur_len, (uint32_t)cur_stride, ch, nchunk, dst);
+                       (uint32_t)cur_len, (uint32_t)cur_stride, ch, nchunk, dst, mask);
     HIPCHK(hipGetLastError());
     if (nchunk == 1) break;
+    mask = nullptr;  // later passes multiply partial products
     // next round: group g's partials are contiguous at g*nchunk
     gm = GroupMap{1, 1, 0, 0, nchunk};
     src = dst;
@@ -670,12 +706,17 @@ extern "C" int eg_fixed_base_destroy(eg_fixed_base* fb) {
   return EG_OK;
 }
 
+static void coalescer_stop(eg_ctx* c);  // eg_capi_coalesce.inc
+
 extern "C" int eg_ctx_destroy(eg_ctx* c) {
   if (!c) return EG_OK;
+  coalescer_stop(c);  // drains pending per-element calls first
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   eg_fixed_base_destroy(c->gtab);
   eg_fixed_base_destroy(c->Ktab);
+  eg_fixed_base_destroy(c->g_ct);
+  eg_fixed_base_destroy(c->K_ct);
   for (auto& kv : c->share_keys) eg_fixed_base_destroy(kv.second);
   for (auto& b : c->ws)
     if (b.ptr) hipFree(b.ptr);
@@ -683,10 +724,10 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
     if (kv.second.ptr) hipFree(kv.second.ptr);
   for (auto& kv : c->sched) hipFree(const_cast<uint32_t*>(kv.second.ptr));
   for (auto& r : c->prof) {  // a profile window left open
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
-    if (r.d_clk) hipFree(r.d_clk);
+    if (r.a) hipEventDestroy(r.a);
+    if (r.b) hipEventDestroy(r.b);
   }
+  if (c->d_clk) hipFree(c->d_clk);
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);
@@ -820,11 +861,17 @@ extern "C" int eg_multinv_batch(eg_ctx* c, const uint8_t* a_be, uint8_t* out_be,
   return pow_host(c, a_be, e, 512, true, out_be, n, nullptr);
 }
 
+static int multp_host(eg_ctx* c, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be, size_t n);
+
 extern "C" int eg_multp_batch(eg_ctx* c, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be, size_t n) {
   if (!c || (n && (!a_be || !b_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
   if (!n) return EG_OK;
   if (n > kMaxBatch) return fail(EG_ERR_ARG, "batch too large");
   Locked L(c);
+  return multp_host(c, a_be, b_be, out_be, n);
+}
+
+static int multp_host(eg_ctx* c, const uint8_t* a_be, const uint8_t* b_be, uint8_t* out_be, size_t n) {
   uint8_t *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
   uint32_t *ea = nullptr, *eb = nullptr;
   int rc;
@@ -870,24 +917,70 @@ extern "C" int eg_prod_reduce(eg_ctx* c, const uint8_t* elems_be, size_t groups,
   return EG_OK;
 }
 
+// In-kernel clock of a profile window (MI355X_MICROARCH.md 'DVFS give-back' item 6): each record
+// is one workgroup's (s_memtime ticks, s_memrealtime ticks), the latter at a fixed 100 MHz; the
+// clock is the MEDIAN of the per-workgroup ratios.  Records that are unset (0), wrapped (a
+// negative difference reads as >= 2^63), shorter than 10 us (too coarse at 100 MHz) or whose
+// ratio lies outside [0.5, 3.5] GHz are dropped and counted; a window with no usable record
+// yields 0 GHz.  Summing raw ticks instead lets one garbage record dominate the result.
+extern "C" int eg_clock_median(const uint64_t* recs, size_t n, double* ghz, uint32_t* used, uint32_t* dropped) {
+  if ((n && !recs) || !ghz) return fail(EG_ERR_ARG, "null argument");
+  std::vector<double> r;
+  r.reserve(n);
+  uint32_t drop = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t cyc = recs[2 * i], rt = recs[2 * i + 1];
+    if (cyc == 0 || rt < 1000 || cyc >> 62 || rt >> 62) {
+      ++drop;
+      continue;
+    }
+    const double g = (double)cyc / (double)rt * 0.1;  // GHz: ticks per 10 ns real-time tick / 10
+    if (!(g >= 0.5 && g <= 3.5)) {
+      ++drop;
+      continue;
+    }
+    r.push_back(g);
+  }
+  *ghz = 0;
+  if (!r.empty()) {
+    const size_t m = r.size() / 2;
+    std::nth_element(r.begin(), r.begin() + m, r.end());
+    double med = r[m];
+    if (r.size() % 2 == 0) med = 0.5 * (med + *std::max_element(r.begin(), r.begin() + m));
+    *ghz = med;
+  }
+  if (used) *used = (uint32_t)r.size();
+  if (dropped) *dropped = drop;
+  return EG_OK;
+}
+
+static void prof_clear(eg_ctx* c) {
+  for (auto& r : c->prof) {
+    if (r.a) hipEventDestroy(r.a);
+    if (r.b) hipEventDestroy(r.b);
+  }
+  c->prof.clear();
+}
+
 extern "C" int eg_ctx_profile_begin(eg_ctx* c) {
   if (!c) return fail(EG_ERR_ARG, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
-  HIPCHK(hipStreamSynchronize(c->stream));  // a pending window's launches may still write d_clk
-  for (auto& r : c->prof) {
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
-    if (r.d_clk) hipFree(r.d_clk);
-  }
-  c->prof.clear();
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));  // a pending window's launches may still write the records
+  prof_clear(c);
+  if (!c->d_clk) HIPCHK(hipMalloc(&c->d_clk, kClockRecs * 2 * sizeof(uint64_t)));
+  HIPCHK(hipMemsetAsync(c->d_clk, 0, kClockRecs * 2 * sizeof(uint64_t), c->stream));
+  c->clk_used = 0;
   c->timing = true;
   return EG_OK;
 }
 
-extern "C" int eg_ctx_profile_clock(eg_ctx* c, double* ghz) {
+extern "C" int eg_ctx_profile_clock(eg_ctx* c, double* ghz, uint32_t* used, uint32_t* dropped) {
   if (!c || !ghz) return fail(EG_ERR_ARG, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   *ghz = c->prof_clock_ghz;
+  if (used) *used = c->clk_used_last;
+  if (dropped) *dropped = c->clk_dropped_last;
   return EG_OK;
 }
 
@@ -896,47 +989,36 @@ extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  double t = 0, m = 0, sq = 0, cyc = 0, wall = 0;
+  double t = 0, m = 0, sq = 0;
   for (auto& r : c->prof) {
     float x = 0;
     HIPCHK(hipEventElapsedTime(&x, r.a, r.b));
     t += x;
     m += r.mm;
     sq += r.sqr;
-    if (r.d_clk) {
-      std::vector<uint64_t> h((size_t)r.nblocks * 2);
-      HIPCHK(hipMemcpy(h.data(), r.d_clk, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-      uint32_t unset = 0;
-      for (uint32_t b = 0; b < r.nblocks; ++b) {
-        if (h[2 * b + 1] == 0) {  // workgroup record not written (must not happen)
-          ++unset;
-          continue;
-        }
-        cyc += (double)h[2 * b];
-        wall += (double)h[2 * b + 1];
-      }
-      if (unset && getenv("EG_DEBUG_CLK"))
-        fprintf(stderr, "eg_ctx_profile_end: %u of %u workgroup clock records unset\n", unset, r.nblocks);
-      hipFree(r.d_clk);
-    }
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
   }
-  int wall_khz = 0;
   c->prof_clock_ghz = 0;
-  if (wall > 0 && hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess &&
-      wall_khz > 0)
-    c->prof_clock_ghz = cyc / (wall / ((double)wall_khz * 1e3)) / 1e9;
+  c->clk_used_last = c->clk_dropped_last = 0;
+  if (c->d_clk && c->clk_used) {
+    std::vector<uint64_t> h(c->clk_used * 2);
+    HIPCHK(hipMemcpy(h.data(), c->d_clk, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    eg_clock_median(h.data(), c->clk_used, &c->prof_clock_ghz, &c->clk_used_last, &c->clk_dropped_last);
+    if (c->clk_dropped_last && getenv("EG_DEBUG_CLK"))
+      fprintf(stderr, "eg_ctx_profile_end: %u of %zu workgroup clock records dropped\n", c->clk_dropped_last,
+              c->clk_used);
+  }
   if (ms) *ms = t;
   if (mm) *mm = m;
   if (sqr) *sqr = sq;
   if (launches) *launches = (int)c->prof.size();
-  c->prof.clear();
+  prof_clear(c);
+  c->clk_used = 0;
   c->timing = false;
   return EG_OK;
 }
 
 #include "eg_capi_ballot.inc"
+#include "eg_capi_coalesce.inc"
 
 // ------------------------------------------------------------------------------
 // device-pointer powP / fixed-base powP (asynchronous on the ctx stream): the

@@ -384,6 +384,8 @@ struct PowShape {
   uint32_t rows;       // Lim-Lee rows h of a plain comb (0: kCombH = 5 rows of 52 bits, 32-entry
                        // tables; 4: rows of 64 bits, 16-entry tables -- the constant-time trustee
                        // pair, whose masked scans read every entry of a table)
+  uint32_t fb_small[2][2];  // fixed-base term [o][t] whose scalar is < 2^wbits (the vote m of
+                            // beta = K^R g^m): only radix window 0 is applied (host schedule only)
 };
 
 // Constant-time table read for secret digits (k_pow<F, CT = true>, the trustee's shares):
@@ -490,9 +492,11 @@ struct PowPart {
 };
 
 // CT = true: the constant-time instantiation for secret exponents (trustee shares s_i and
-// P_l(x_i), proof nonces u).  Comb shapes only (no 4-bit window, no radix fixed-base terms):
-// every comb-table read is ct_select_to_lds over all 32 entries, and the square/multiply
-// schedule is the comb's fixed one, so neither time nor addresses depend on exponent bits.
+// P_l(x_i), proof nonces u; encryption nonces R, u and the vote with eg_ctx_set_ct_encrypt).
+// Comb shapes and small-window radix fixed-base terms (no 4-bit window): every comb-table read
+// is ct_select_to_lds over the block's whole table, every fixed-base read over the window's
+// whole column, and the square/multiply schedule is fixed by the shape, so neither time nor
+// addresses depend on exponent bits.
 template <bool F, bool CT>
 __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowPart P0,
                                                 PowPart P1, const uint32_t* __restrict__ elems,
@@ -500,9 +504,10 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
                                                 uint32_t* __restrict__ out, FbTab fb0, FbTab fb1,
                                                 uint64_t* __restrict__ clk) {
   __shared__ uint8_t s_dig[kGroupsPerBlock][64];
-  // clk (profiling only): per workgroup, shader-clock cycles and constant-rate wall ticks
-  // from its start to its end, so the host can report the clock the launch ran at
-  const uint64_t cyc0 = clk ? clock64() : 0, wall0 = clk ? wall_clock64() : 0;
+  // clk (profiling only): per workgroup, shader-clock ticks (s_memtime) and 100 MHz real-time
+  // ticks (s_memrealtime) from its start to its end; the host reports the median per-workgroup
+  // ratio (eg_clock_median), the in-kernel clock of MI355X_MICROARCH.md 'DVFS give-back' item 6
+  const uint64_t cyc0 = clk ? __builtin_amdgcn_s_memtime() : 0, wall0 = clk ? __builtin_amdgcn_s_memrealtime() : 0;
   const bool second = blockIdx.x >= P0.nblocks;
   const PowPart& P = second ? P1 : P0;  // kernarg memory: shape fields stay scalar loads
   const PowShape& S = P.S;
@@ -529,6 +534,8 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   // Outer loop: one Montgomery multiply (or square) per trip, at a single inlined site; the
   // inner loop runs the program's loads, stores and digit spreads up to the next multiply.
   uint32_t pc = 0;
+  const uint32_t* fb_col = nullptr;  // CT: the fixed-base window column being scanned
+  uint32_t fb_h = 0, fb_d = 0;
   while (true) {
     const uint32_t* ysrc = nullptr;  // nullptr: square
     uint32_t kind = OP_END, arg = 0;
@@ -555,6 +562,19 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         const uint32_t kf = arg & 255u;
         const uint32_t d = be_digit(scalars + (size_t)J[5 + 2 * ((arg >> 9) & 1u) + ((arg >> 8) & 1u)] * 32, 32,
                                     kf * T.wbits, T.wbits);
+        if constexpr (CT) {
+          // secret scalar (encryption nonces, the vote): masked scan of the window's whole
+          // column of 2^wbits entries (small tables only, eg_ctx_set_ct_encrypt)
+          fb_col = T.data + (size_t)(kf << T.wbits) * kW;
+          fb_h = T.wbits;
+          fb_d = d;
+          if (kind == OP_MUL_FB) { ysrc = fb_col; break; }
+          ct_select_to_lds(slot, fb_col, fb_h, fb_d);
+          wave_sync();
+          load_elem(x, slot);
+          wave_sync();
+          continue;
+        }
         const uint32_t* ent = T.data + ((size_t)(kf << T.wbits) + d) * kW;
         if (kind == OP_MUL_FB) { ysrc = ent; break; }
         load_elem(x, ent);
@@ -614,6 +634,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     if (ysrc) {
       if constexpr (CT) {
         if (kind == OP_MUL_COMB) ct_select_to_lds(slot, tbl, ch, dig[arg]);  // secret digit
+        else if (kind == OP_MUL_FB) ct_select_to_lds(slot, fb_col, fb_h, fb_d);
         else elem_to_lds(slot, ysrc);
       } else {
         elem_to_lds(slot, ysrc);
@@ -628,8 +649,8 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
     wave_sync();
   }
   if (clk && threadIdx.x == 0) {
-    clk[2 * (size_t)blockIdx.x] = clock64() - cyc0;
-    clk[2 * (size_t)blockIdx.x + 1] = wall_clock64() - wall0;
+    clk[2 * (size_t)blockIdx.x] = __builtin_amdgcn_s_memtime() - cyc0;
+    clk[2 * (size_t)blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - wall0;
   }
 }
 
@@ -639,6 +660,9 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
 // and its k-th element sits at offset(g) + k*stride.  Job j -> group j / nchunk,
 // chunk j % nchunk; every job runs exactly `chunk`-1 multiplies (missing elements
 // are R mod p, the Montgomery one) so all groups of a wave stay in lock-step.
+// mask (optional): element k of every group takes part only if mask[k] != 0, else it counts
+// as the Montgomery one (the tally over CAST ballots: k = ballot, mask = the cast flags); the
+// selection only picks the operand's address, so the wave stays uniform.
 // ---------------------------------------------------------------------------------
 struct GroupMap {
   uint32_t R0, R1, M0, M1, M2;
@@ -653,7 +677,8 @@ template <bool F>
 __global__ void __launch_bounds__(kBlock) k_prod(const MontConsts* __restrict__ C,
                                                  const uint32_t* __restrict__ in, GroupMap gm, uint32_t ngroups,
                                                  uint32_t len, uint32_t stride, uint32_t chunk,
-                                                 uint32_t nchunk, uint32_t* __restrict__ out) {
+                                                 uint32_t nchunk, uint32_t* __restrict__ out,
+                                                 const uint8_t* __restrict__ mask) {
   const uint32_t gid = group_id();
   const uint32_t njobs = ngroups * nchunk;
   const uint32_t jb = gid < njobs ? gid : njobs - 1;
@@ -664,11 +689,13 @@ __global__ void __launch_bounds__(kBlock) k_prod(const MontConsts* __restrict__ 
   uint32_t x[kL];
   const size_t base = gm.offset(g);
   const uint32_t k0 = c * chunk;
-  load_elem(x, in + (base + (size_t)k0 * stride) * kW);
+  const bool in0 = k0 < len && (mask == nullptr || mask[k0] != 0);
+  load_elem(x, in0 ? in + (base + (size_t)k0 * stride) * kW : C->one);
 #pragma unroll 1
   for (uint32_t k = 1; k < chunk; ++k) {
     const uint32_t kk = k0 + k;
-    const uint32_t* E = kk < len ? in + (base + (size_t)kk * stride) * kW : C->one;
+    const bool use = kk < len && (mask == nullptr || mask[kk] != 0);
+    const uint32_t* E = use ? in + (base + (size_t)kk * stride) * kW : C->one;
     mmul_g(M, x, slot, E);
   }
   if (gid < njobs) store_elem(out + (size_t)gid * kW, x);
@@ -799,13 +826,12 @@ __device__ __forceinline__ U256 mulsmall_mod(const U256& a, uint32_t L, const U2
   }
   return x;
 }
-__device__ __forceinline__ U256 negmod(const U256& a, const U256& q) {
-  bool z = true;
-  for (int i = 0; i < 8; ++i) z &= (a.w[i] == 0);
-  if (z) return a;
+__device__ __forceinline__ U256 negmod(const U256& a, const U256& q) {  // (q - a) mod q, branch-free
+  uint32_t nz = 0;
+  for (int i = 0; i < 8; ++i) nz |= a.w[i];
   U256 r = q;
   sub256(r, a);
-  return r;
+  return sel256(0u - (uint32_t)(nz != 0), r, a);
 }
 
 // (a - b) mod q for a, b < q
@@ -841,7 +867,7 @@ __global__ void k_enc_prep(const uint8_t* __restrict__ q_be, const uint8_t* __re
   const U256 vf = ld256(nonces + ((size_t)i * 4 + 3) * 32);
   const uint32_t m = votes[i] ? 1u : 0u;
   const U256 sf = addmod256(vf, mulmod256(R, cf, q), q);
-  const U256 sg = m ? cf : negmod(cf, q);
+  const U256 sg = sel256(0u - m, cf, negmod(cf, q));  // m ? c_fake : -c_fake, branch-free (secret vote)
   U256 ms;
   for (int k = 0; k < 8; ++k) ms.w[k] = 0;
   ms.w[0] = m;
@@ -877,11 +903,30 @@ __global__ void k_enc_finish(const uint8_t* __restrict__ q_be, const uint8_t* __
   const U256 cr = submod256(c, cf, q);
   const U256 vr = submod256(u, mulmod256(cr, R, q), q);
   uint8_t* o = rproof + (size_t)i * 4 * 32;
-  if (votes[i]) {
-    st256(o + 0, cf); st256(o + 32, vf); st256(o + 64, cr); st256(o + 96, vr);
-  } else {
-    st256(o + 0, cr); st256(o + 32, vr); st256(o + 64, cf); st256(o + 96, vf);
-  }
+  const uint32_t mk = 0u - (uint32_t)(votes[i] != 0);  // the branch order follows the vote: masked
+  st256(o + 0, sel256(mk, cf, cr));
+  st256(o + 32, sel256(mk, vf, vr));
+  st256(o + 64, sel256(mk, cr, cf));
+  st256(o + 96, sel256(mk, vr, vf));
+}
+
+// Encryption commitments are computed vote-independently, real branch (a, b) in slots 0-1 and
+// the simulated branch in slots 2-3 of each selection's 4 commitment elements; this puts them in
+// proof order (branch 0 first), i.e. swaps the pairs where the vote is 1, with masks (the vote
+// is secret).  One thread per 4-word column of a selection's pair.
+__global__ void k_enc_order(uint32_t* __restrict__ comm, const uint8_t* __restrict__ votes, uint32_t n) {
+  constexpr uint32_t kQuads = 2 * kW / 4;  // a pair of elements, in uint4
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * kQuads) return;
+  const uint32_t i = (uint32_t)(t / kQuads), k = (uint32_t)(t % kQuads);
+  const uint32_t mk = 0u - (uint32_t)(votes[i] != 0);
+  uint4* lo = reinterpret_cast<uint4*>(comm + (size_t)i * 4 * kW) + k;
+  uint4* hi = lo + kQuads;
+  const uint4 a = *lo, b = *hi;
+  *lo = make_uint4((a.x & ~mk) | (b.x & mk), (a.y & ~mk) | (b.y & mk), (a.z & ~mk) | (b.z & mk),
+                   (a.w & ~mk) | (b.w & mk));
+  *hi = make_uint4((b.x & ~mk) | (a.x & mk), (b.y & ~mk) | (a.y & mk), (b.z & ~mk) | (a.z & mk),
+                   (b.w & ~mk) | (a.w & mk));
 }
 
 // Generic response v = u - c*x mod q (x per item or shared when x_stride == 0);

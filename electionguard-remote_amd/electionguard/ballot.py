@@ -90,15 +90,21 @@ def _ptr(a: np.ndarray):
 
 
 class ElectionKey:
-    """Registers the joint election key K (fixed-base table) on a GroupContext."""
+    """The joint election key K: registers its fixed-base table (window_bits wide) on a
+    GroupContext.  Every ballot call passes K itself, and the library sets it under the ctx lock
+    for that call, so threads using different keys on one shared context cannot mix them up."""
 
     def __init__(self, group: GroupContext, K: int, window_bits: int = 8):
         self.group, self.K, self.window_bits = group, int(K), window_bits
         self._K_be = p_bytes(K)
-        native.check(group._lib, "eg_set_election_key",
-                     group._lib.eg_set_election_key(group.handle, native.buf(self._K_be), window_bits))
+        self.ensure()
+
+    @property
+    def K_be(self) -> bytes:
+        return self._K_be
 
     def ensure(self) -> None:
+        """(Re)build K's table at this key's width (a no-op when the ctx already holds it)."""
         native.check(self.group._lib, "eg_set_election_key",
                      self.group._lib.eg_set_election_key(self.group.handle, native.buf(self._K_be),
                                                          self.window_bits))
@@ -119,11 +125,11 @@ def batch_encryption(group: GroupContext, key: ElectionKey, qbar: int, man: Mani
     rp = np.empty((nb, man.nsel, 4, 32), dtype=np.uint8)
     cp = np.empty((nb, man.n_contests, 2, 32), dtype=np.uint8)
     if nb:
-        key.ensure()
         qb = q_bytes(qbar)
         native.check(group._lib, "eg_encrypt_ballots",
-                     group._lib.eg_encrypt_ballots(group.handle, native.buf(qb), nb, man.n_contests, man.spc,
-                                                   _ptr(votes), _ptr(sn), _ptr(cn), _ptr(cts), _ptr(rp), _ptr(cp)))
+                     group._lib.eg_encrypt_ballots(group.handle, native.buf(key.K_be), native.buf(qb), nb,
+                                                   man.n_contests, man.spc, _ptr(votes), _ptr(sn), _ptr(cn), _ptr(cts),
+                                                   _ptr(rp), _ptr(cp)))
     return EncryptedBallots(cts, rp, cp)
 
 
@@ -133,11 +139,10 @@ def batch_encryption_device(group: GroupContext, key: ElectionKey, qbar: int, ma
     """batch_encryption on device pointers (e.g. torch tensors' data_ptr()): the same
     layouts, inputs and outputs resident in HBM (eg_encrypt_ballots_dev)."""
     if nb:
-        key.ensure()
         native.check(group._lib, "eg_encrypt_ballots_dev",
-                     group._lib.eg_encrypt_ballots_dev(group.handle, native.buf(q_bytes(qbar)), nb, man.n_contests,
-                                                       man.spc, d_votes, d_sel_nonces, d_contest_nonces, d_cts,
-                                                       d_rproof, d_cproof))
+                     group._lib.eg_encrypt_ballots_dev(group.handle, native.buf(key.K_be), native.buf(q_bytes(qbar)),
+                                                       nb, man.n_contests, man.spc, d_votes, d_sel_nonces,
+                                                       d_contest_nonces, d_cts, d_rproof, d_cproof))
 
 
 class Verifier:
@@ -147,37 +152,47 @@ class Verifier:
         self.group, self.key, self.qbar, self.man = group, key, int(qbar), man
         self._qb = q_bytes(qbar)
 
-    def verify(self, eb: EncryptedBallots, with_tally: bool = True) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray]]:
-        """-> ok_sel (nb, nsel) bool, ok_contest (nb, nc) bool, tally (n_real, 2, 512) or None."""
+    def verify(self, eb: EncryptedBallots, with_tally: bool = True,
+               cast: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray]]:
+        """-> ok_sel (nb, nsel) bool, ok_contest (nb, nc) bool, tally (n_real, 2, 512) or None.
+
+        cast (nb,) bool (None = all cast): every ballot is verified, only the cast ones are
+        tallied (runAccumulateBallots counts cast ballots; spoiled ones are decrypted one by one,
+        RunRemoteDecryptor.java:264-269)."""
         man, g = self.man, self.group
         nb = eb.n
         cts = np.ascontiguousarray(eb.cts, dtype=np.uint8)
         rp = np.ascontiguousarray(eb.rproof, dtype=np.uint8)
         cp = np.ascontiguousarray(eb.cproof, dtype=np.uint8)
+        cm = None if cast is None else np.ascontiguousarray(np.asarray(cast).reshape(nb) != 0, dtype=np.uint8)
         ok_s = np.zeros((nb, man.nsel), dtype=np.uint8)
         ok_c = np.zeros((nb, man.n_contests), dtype=np.uint8)
         tally = np.empty((man.n_real, 2, 512), dtype=np.uint8) if with_tally else None
-        K_be = p_bytes(self.key.K)
         native.check(g._lib, "eg_verify_ballots",
-                     g._lib.eg_verify_ballots(g.handle, native.buf(K_be), native.buf(self._qb), nb, man.n_contests,
-                                              man.spc, man.votes_allowed, man.votes_allowed, _ptr(cts), _ptr(rp),
-                                              _ptr(cp), _ptr(ok_s), _ptr(ok_c),
-                                              _ptr(tally) if tally is not None else None))
+                     g._lib.eg_verify_ballots(g.handle, native.buf(self.key.K_be), native.buf(self._qb), nb,
+                                              man.n_contests, man.spc, man.votes_allowed, man.votes_allowed, _ptr(cts),
+                                              _ptr(rp), _ptr(cp), _ptr(cm) if cm is not None else None, _ptr(ok_s),
+                                              _ptr(ok_c), _ptr(tally) if tally is not None else None))
         return ok_s.astype(bool), ok_c.astype(bool), tally
 
     def verify_device(self, d_cts: int, d_rproof: int, d_cproof: int, nb: int, d_ok_sel: int, d_ok_con: int,
-                      d_tally: Optional[int]) -> None:
-        """Asynchronous verify on device pointers (e.g. torch CUDA tensors' data_ptr())."""
+                      d_tally: Optional[int], d_cast: Optional[int] = None) -> None:
+        """Asynchronous verify on device pointers (e.g. torch CUDA tensors' data_ptr()); d_cast
+        (nb bytes, 0 = spoiled) as verify's cast."""
         man, g = self.man, self.group
-        self.key.ensure()  # the ctx may hold another key since this Verifier was made (no-op if not)
         native.check(g._lib, "eg_verify_ballots_dev",
-                     g._lib.eg_verify_ballots_dev(g.handle, native.buf(self._qb), nb, man.n_contests, man.spc,
-                                                  man.votes_allowed, man.votes_allowed, d_cts, d_rproof, d_cproof,
-                                                  d_ok_sel, d_ok_con, d_tally))
+                     g._lib.eg_verify_ballots_dev(g.handle, native.buf(self.key.K_be), native.buf(self._qb), nb,
+                                                  man.n_contests, man.spc, man.votes_allowed, man.votes_allowed, d_cts,
+                                                  d_rproof, d_cproof, d_cast, d_ok_sel, d_ok_con, d_tally))
 
 
-def accumulate_tally(group: GroupContext, man: Manifest, eb: EncryptedBallots) -> np.ndarray:
-    """runAccumulateBallots without verification: per real selection, prod pad / prod data."""
+def accumulate_tally(group: GroupContext, man: Manifest, eb: EncryptedBallots,
+                     cast: Optional[np.ndarray] = None) -> np.ndarray:
+    """runAccumulateBallots without verification: per real selection, prod pad / prod data over the
+    cast ballots (cast (nb,) bool, None = all)."""
+    if cast is not None:
+        eb = EncryptedBallots(eb.cts[np.asarray(cast, bool)], eb.rproof[np.asarray(cast, bool)],
+                              eb.cproof[np.asarray(cast, bool)])
     nb = eb.n
     sel = eb.cts.reshape(nb, man.n_contests, man.spc, 2, 512)[:, :, : man.n_selections]
     # groups ordered (contest, selection, component), elements over ballots

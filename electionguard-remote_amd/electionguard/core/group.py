@@ -58,6 +58,26 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _p_be(x) -> bytes:
+    if isinstance(x, ElementModP):
+        return x.byteArray()
+    if isinstance(x, (bytes, bytearray)):
+        if len(x) != P_BYTES:
+            raise ValueError("ElementModP bytes must be 512 long")
+        return bytes(x)
+    return p_bytes(int(x))
+
+
+def _q_be(x) -> bytes:
+    if isinstance(x, ElementModQ):
+        return x.byteArray()
+    if isinstance(x, (bytes, bytearray)):
+        if len(x) != Q_BYTES:
+            raise ValueError("ElementModQ bytes must be 32 long")
+        return bytes(x)
+    return q_bytes(int(x))
+
+
 # Algorithmic 32-bit MACs of one 4096-bit (128-word) Montgomery operation:
 # product 128^2 (a square needs only 128*129/2) + reduction 128^2.
 MAC_PER_MUL = 2 * 128 * 128
@@ -71,7 +91,9 @@ class KernelProfile:
     mont_ops: float    # Montgomery multiplies + squarings
     squarings: float   # of which squarings
     launches: int
-    clock_ghz: float = 0.0  # shader clock the launches ran at (per-workgroup clock64 / wall_clock64)
+    clock_ghz: float = 0.0  # shader clock the launches ran at (median per-workgroup s_memtime / s_memrealtime)
+    clock_records: int = 0  # workgroup clock records behind clock_ghz
+    clock_dropped: int = 0  # records dropped as unset, wrapped or out of range (eg_clock_median)
 
     @property
     def macs(self) -> float:
@@ -191,13 +213,41 @@ class GroupContext:
                          self._lib.eg_multinv_batch(self._ctx, _ptr(A), _ptr(out), len(A)))
         return out
 
-    # ---- per-element convenience (batches of one) ----
+    # ---- per-element API: coalesced across calling threads (eg_*_one, include/eg_hip.h) ----
+    # The reference calls the group element by element from 11 threads (RunRemoteWorkflowTest.java:
+    # 140,180); concurrent calls join one GPU batch (eg_ctx_set_coalescing sets its window).
+    def powP_one(self, base, e) -> bytes:
+        b, x = _p_be(base), _q_be(e)
+        out = bytearray(P_BYTES)
+        native.check(self._lib, "eg_powp_one",
+                     self._lib.eg_powp_one(self._ctx, native.buf(b), native.buf(x), native.buf(out)))
+        return bytes(out)
+
+    def gPowP_one(self, e) -> bytes:
+        x = _q_be(e)
+        out = bytearray(P_BYTES)
+        native.check(self._lib, "eg_gpowp_one", self._lib.eg_gpowp_one(self._ctx, native.buf(x), native.buf(out)))
+        return bytes(out)
+
+    def multP_one(self, a, b) -> bytes:
+        x, y = _p_be(a), _p_be(b)
+        out = bytearray(P_BYTES)
+        native.check(self._lib, "eg_multp_one",
+                     self._lib.eg_multp_one(self._ctx, native.buf(x), native.buf(y), native.buf(out)))
+        return bytes(out)
+
+    def set_coalescing(self, max_batch: int, window_us: int) -> None:
+        native.check(self._lib, "eg_ctx_set_coalescing",
+                     self._lib.eg_ctx_set_coalescing(self._ctx, max_batch, window_us))
+
     def gPowP(self, e: Union["ElementModQ", int]) -> "ElementModP":
-        return ElementModP.from_bytes(self.gPowP_batch([e])[0], self)
+        return ElementModP.from_bytes(self.gPowP_one(e), self)
 
     def multP(self, *elems: "ElementModP") -> "ElementModP":
         if not elems:
             return self.ONE_MOD_P
+        if len(elems) == 2:
+            return ElementModP.from_bytes(self.multP_one(elems[0], elems[1]), self)
         return ElementModP.from_bytes(self.prodP_groups(list(elems), 1, len(elems))[0], self)
 
     def dLogG(self, y: "ElementModP", max_result: int) -> Optional[int]:
@@ -222,6 +272,18 @@ class GroupContext:
         native.check(self._lib, "eg_ctx_set_hash_format", self._lib.eg_ctx_set_hash_format(self._ctx, FORMATS[fmt]))
         self._hash_format = fmt
 
+    # ---- constant-time encryption (eg_ctx_set_ct_encrypt) ----
+    @property
+    def ct_encrypt(self) -> bool:
+        """Encryption with masked scans of small radix tables: no address or schedule depends on
+        a nonce or a vote (the default indexes the wide tables by nonce digits).  Same bytes."""
+        return getattr(self, "_ct_encrypt", False)
+
+    @ct_encrypt.setter
+    def ct_encrypt(self, on: bool) -> None:
+        native.check(self._lib, "eg_ctx_set_ct_encrypt", self._lib.eg_ctx_set_ct_encrypt(self._ctx, 1 if on else 0))
+        self._ct_encrypt = bool(on)
+
     # ---- profiling of the dominant kernel ----
     def profile_begin(self) -> None:
         native.check(self._lib, "eg_ctx_profile_begin", self._lib.eg_ctx_profile_begin(self._ctx))
@@ -231,9 +293,11 @@ class GroupContext:
         native.check(self._lib, "eg_ctx_profile_end",
                      self._lib.eg_ctx_profile_end(self._ctx, ctypes.byref(ms), ctypes.byref(mm), ctypes.byref(sq),
                                                   ctypes.byref(n)))
-        ghz = ctypes.c_double()
-        native.check(self._lib, "eg_ctx_profile_clock", self._lib.eg_ctx_profile_clock(self._ctx, ctypes.byref(ghz)))
-        return KernelProfile(ms.value, mm.value, sq.value, n.value, ghz.value)
+        ghz, used, dropped = ctypes.c_double(), ctypes.c_uint32(), ctypes.c_uint32()
+        native.check(self._lib, "eg_ctx_profile_clock",
+                     self._lib.eg_ctx_profile_clock(self._ctx, ctypes.byref(ghz), ctypes.byref(used),
+                                                    ctypes.byref(dropped)))
+        return KernelProfile(ms.value, mm.value, sq.value, n.value, ghz.value, used.value, dropped.value)
 
     def sync(self) -> None:
         native.check(self._lib, "eg_ctx_sync", self._lib.eg_ctx_sync(self._ctx))
@@ -292,10 +356,10 @@ class ElementModP:
         return p_bytes(self.value)
 
     def powP(self, e: Union["ElementModQ", int]) -> "ElementModP":
-        return ElementModP.from_bytes(self.group.powP_batch([self], [e])[0], self.group)
+        return ElementModP.from_bytes(self.group.powP_one(self, e), self.group)
 
     def times(self, other: "ElementModP") -> "ElementModP":
-        return ElementModP.from_bytes(self.group.multP_batch([self], [other])[0], self.group)
+        return ElementModP.from_bytes(self.group.multP_one(self, other), self.group)
 
     def multInv(self) -> "ElementModP":
         return ElementModP.from_bytes(self.group.multInv_batch([self])[0], self.group)

@@ -23,7 +23,9 @@ EXPORTED = [
     "eg_powp_batch_dev", "eg_fb_pow_batch_dev",
     "eg_multp_batch", "eg_prod_reduce", "eg_multinv_batch", "eg_verify_ballots",
     "eg_set_election_key", "eg_verify_ballots_dev", "eg_encrypt_ballots", "eg_encrypt_ballots_dev",
-    "eg_trustee_decrypt_batch", "eg_verify_shares",
+    "eg_trustee_decrypt_batch", "eg_verify_shares", "eg_clock_median",
+    "eg_ctx_set_coalescing", "eg_powp_submit", "eg_gpowp_submit", "eg_multp_submit", "eg_ticket_wait",
+    "eg_powp_one", "eg_gpowp_one", "eg_multp_one", "eg_ctx_set_ct_encrypt",
 ]
 
 
@@ -58,7 +60,8 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_ctx_sync": ([P], I),
         "eg_ctx_profile_begin": ([P], I),
         "eg_ctx_profile_end": ([P, D, D, D, ctypes.POINTER(I)], I),
-        "eg_ctx_profile_clock": ([P, D], I),
+        "eg_ctx_profile_clock": ([P, D, ctypes.POINTER(U32), ctypes.POINTER(U32)], I),
+        "eg_clock_median": ([P, S, D, ctypes.POINTER(U32), ctypes.POINTER(U32)], I),
         "eg_ctx_g_table": ([P], P),
         "eg_ctx_set_hash_format": ([P, I], I),
         "eg_fixed_base_create": ([P, P, I, ctypes.POINTER(c_vp)], I),
@@ -70,11 +73,20 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_multp_batch": ([P, P, P, P, S], I),
         "eg_prod_reduce": ([P, P, S, S, P], I),
         "eg_multinv_batch": ([P, P, P, S], I),
-        "eg_verify_ballots": ([P, P, P, S, S, S, S, U32, P, P, P, P, P, P], I),
+        "eg_verify_ballots": ([P, P, P, S, S, S, S, U32, P, P, P, P, P, P, P], I),
         "eg_set_election_key": ([P, P, I], I),
-        "eg_verify_ballots_dev": ([P, P, S, S, S, S, U32, P, P, P, P, P, P], I),
-        "eg_encrypt_ballots": ([P, P, S, S, S, P, P, P, P, P, P], I),
-        "eg_encrypt_ballots_dev": ([P, P, S, S, S, P, P, P, P, P, P], I),
+        "eg_verify_ballots_dev": ([P, P, P, S, S, S, S, U32, P, P, P, P, P, P, P], I),
+        "eg_encrypt_ballots": ([P, P, P, S, S, S, P, P, P, P, P, P], I),
+        "eg_encrypt_ballots_dev": ([P, P, P, S, S, S, P, P, P, P, P, P], I),
+        "eg_ctx_set_ct_encrypt": ([P, I], I),
+        "eg_ctx_set_coalescing": ([P, S, U32], I),
+        "eg_powp_submit": ([P, P, P, P, ctypes.POINTER(c_vp)], I),
+        "eg_gpowp_submit": ([P, P, P, ctypes.POINTER(c_vp)], I),
+        "eg_multp_submit": ([P, P, P, P, ctypes.POINTER(c_vp)], I),
+        "eg_ticket_wait": ([P], I),
+        "eg_powp_one": ([P, P, P, P], I),
+        "eg_gpowp_one": ([P, P, P], I),
+        "eg_multp_one": ([P, P, P, P], I),
         "eg_trustee_decrypt_batch": ([P, P, P, P, P, S, P, P], I),
         "eg_verify_shares": ([P, P, P, P, P, P, S, P], I),
     }

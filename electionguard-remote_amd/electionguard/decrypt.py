@@ -15,7 +15,9 @@ and served by ``RunRemoteDecryptingTrustee.directDecrypt`` / ``compensatedDecryp
 
 The mediator side restates ``Decryption.decrypt`` (RunRemoteDecryptor.java:261-262):
 verify each share's proof, Lagrange-combine compensated shares, M = prod M_i,
-T = B / M, t = dLog_g(T) (baby-step giant-step on the GPU).
+T = B / M, t = dLog_g(T) (baby-step giant-step on the GPU), and ``decryptBallot`` for the
+spoiled ballots (RunRemoteDecryptor.java:264-269): the same shares, combine and dLog per
+selection, with every spoiled ballot's selections in ONE trustee batch per guardian.
 """
 from __future__ import annotations
 
@@ -228,6 +230,14 @@ class DecryptionRecord:
     counts: List[Optional[int]]
 
 
+def spoiled_texts(man, cts: np.ndarray) -> np.ndarray:
+    """The real selections' ciphertexts of spoiled ballots, ballot-major: (nb * n_real, 2, 512)
+    from the wire layout (nb, nsel, 2, 512) (placeholders are not part of a decrypted ballot)."""
+    nb = cts.shape[0]
+    sel = np.asarray(cts).reshape(nb, man.n_contests, man.spc, 2, 512)[:, :, : man.n_selections]
+    return np.ascontiguousarray(sel).reshape(nb * man.n_real, 2, 512)
+
+
 class Decryption:
     """Mediator combine (``new Decryption(group, init, trustees, missing).decrypt(tally)``)."""
 
@@ -280,6 +290,31 @@ class Decryption:
         Tv = G.multP_batch(np.ascontiguousarray(T[:, 1]), G.multInv_batch(M))
         rec.counts = dlog_g_batch(G, Tv, max_count)
         return rec
+
+    # ---- spoiled ballots: decryptBallot (RunRemoteDecryptor.java:264-269) ----
+    def decrypt_ballots_record(self, ballots, man) -> DecryptionRecord:
+        """decryptBallot over a batch of spoiled ballots keeping every share and proof: the texts
+        are the ballots' real selections, ballot-major, in ONE trustee batch per guardian (and
+        per missing guardian), so the record's counts are the plaintext selections in that
+        order, each in [0, votesAllowed]."""
+        cts = ballots.cts if hasattr(ballots, "cts") else np.asarray(ballots)
+        return self.decrypt_record(spoiled_texts(man, cts), man.votes_allowed)
+
+    def decryptBallots(self, ballots, man) -> np.ndarray:
+        """-> (nb, n_real) decrypted selections of the spoiled ballots (EncryptedBallots or their
+        (nb, nsel, 2, 512) ciphertexts); -1 where a value is not a valid selection count, which
+        an honest ballot never has."""
+        cts = ballots.cts if hasattr(ballots, "cts") else np.asarray(ballots)
+        nb = cts.shape[0]
+        if nb == 0:
+            return np.zeros((0, man.n_real), dtype=np.int64)
+        counts = self.decrypt_ballots_record(cts, man).counts
+        return np.array([-1 if c is None else int(c) for c in counts], dtype=np.int64).reshape(nb, man.n_real)
+
+    def decryptBallot(self, ballot, man) -> List[int]:
+        """``decryptBallot(spoiled)`` for ONE ballot (its (nsel, 2, 512) ciphertexts); a batch
+        of spoiled ballots should go through decryptBallots (one trustee batch for all)."""
+        return [int(x) for x in self.decryptBallots(np.asarray(ballot).reshape(1, man.nsel, 2, 512), man)[0]]
 
 
 def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionRecord, public_keys: Dict[str, int],

@@ -34,10 +34,12 @@ def rank_env(rank: int, world: int, port: int, base: Optional[dict] = None) -> d
 
 
 def run_ranks(script: str, argv: Sequence[str], world: int, timeout: Optional[float] = None,
-              env: Optional[dict] = None) -> int:
-    """Run `python script argv...` as `world` rank processes; -> the first non-zero exit
-    status (0 when all ranks succeed).  A rank that fails makes the others' collectives
-    error out; any rank still running after `timeout` seconds is killed."""
+              env: Optional[dict] = None, poll_s: float = 0.2) -> int:
+    """Run `python script argv...` as `world` rank processes; -> 0 when every rank succeeds,
+    else the exit status of the FIRST rank that failed.  Every child is polled: as soon as one
+    exits non-zero the others are killed (a dead rank would otherwise leave its peers blocked
+    in a collective until the watchdog fires), so the caller sees the failing rank's status at
+    once.  Ranks still running after `timeout` seconds are killed and 124 is returned."""
     port = free_port()
     procs: List[subprocess.Popen] = []
     for r in range(world):
@@ -45,18 +47,24 @@ def run_ranks(script: str, argv: Sequence[str], world: int, timeout: Optional[fl
     deadline = None if timeout is None else time.monotonic() + timeout
     rc = 0
     try:
-        for p in procs:
-            left = None if deadline is None else max(1.0, deadline - time.monotonic())
-            code = p.wait(timeout=left)
-            if code != 0 and rc == 0:
-                rc = code
-    except subprocess.TimeoutExpired:
-        rc = 124
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if deadline is not None and time.monotonic() > deadline:
+                rc = 124
+                break
+            time.sleep(poll_s)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-                p.wait()
+        for p in procs:
+            p.wait()
     return rc
 
 

@@ -255,6 +255,10 @@ class RemoteDecryptingTrusteeProxy:
             if resp.error:
                 log.error("%s failed: %s", name, resp.error)
                 return None
+            if len(resp.results) != len(req.text):
+                # a short (or long) batch would pair every later result with the wrong text
+                log.error("%s: %d results for %d texts", name, len(resp.results), len(req.text))
+                return None
             results.extend(resp.results)
         return results
 

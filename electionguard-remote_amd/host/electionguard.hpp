@@ -373,10 +373,33 @@ class GroupContext {
     return unpackP(O, groups);
   }
 
-  // ---- per-element API (batches of one) ----
-  ElementModP gPowP(const ElementModQ& e) const { return gPowPBatch({e})[0]; }
-  ElementModP powP(const ElementModP& b, const ElementModQ& e) const { return powPBatch({b}, {e})[0]; }
-  ElementModP multP(const ElementModP& a, const ElementModP& b) const { return multPBatch({a}, {b})[0]; }
+  // ---- per-element API: the upstream call pattern (one element per call, from many threads,
+  // RunRemoteWorkflowTest.java:140,180); concurrent calls are coalesced into one GPU batch by
+  // the library (eg_powp_one / eg_gpowp_one / eg_multp_one, include/eg_hip.h) ----
+  ElementModP gPowP(const ElementModQ& e) const {
+    const auto eb = e.byteArray();
+    ElementModP out;
+    out.group = this;
+    check(eg_gpowp_one(ctx_, eb.data(), out.be.data()), "eg_gpowp_one");
+    return out;
+  }
+  ElementModP powP(const ElementModP& b, const ElementModQ& e) const {
+    const auto eb = e.byteArray();
+    ElementModP out;
+    out.group = this;
+    check(eg_powp_one(ctx_, b.byteArray(), eb.data(), out.be.data()), "eg_powp_one");
+    return out;
+  }
+  ElementModP multP(const ElementModP& a, const ElementModP& b) const {
+    ElementModP out;
+    out.group = this;
+    check(eg_multp_one(ctx_, a.byteArray(), b.byteArray(), out.be.data()), "eg_multp_one");
+    return out;
+  }
+  // batch window of the per-element calls (eg_ctx_set_coalescing)
+  void setCoalescing(size_t maxBatch, uint32_t windowUs) const {
+    check(eg_ctx_set_coalescing(ctx_, maxBatch, windowUs), "eg_ctx_set_coalescing");
+  }
   ElementModP multP(const std::vector<ElementModP>& xs) const {
     return xs.empty() ? one() : prodPGroups(xs, 1, xs.size())[0];
   }
@@ -849,11 +872,11 @@ inline EncryptedBallots batchEncryption(const GroupContext& G, const ElementModP
   eb.cts.resize(nb * man.nsel() * 2 * EG_P_BYTES);
   eb.rproof.resize(nb * man.nsel() * 4 * 32);
   eb.cproof.resize(nb * man.nContests * 2 * 32);
-  setElectionKey(G, K, windowBits);
+  setElectionKey(G, K, windowBits);  // K's table at this width (the call itself passes K too)
   const auto qb = qbar.byteArray();
   if (nb)
-    check(eg_encrypt_ballots(G.handle(), qb.data(), nb, man.nContests, man.spc(), votes.data(), selNonces.data(),
-                             contestNonces.data(), eb.cts.data(), eb.rproof.data(), eb.cproof.data()),
+    check(eg_encrypt_ballots(G.handle(), K.byteArray(), qb.data(), nb, man.nContests, man.spc(), votes.data(),
+                             selNonces.data(), contestNonces.data(), eb.cts.data(), eb.rproof.data(), eb.cproof.data()),
           "eg_encrypt_ballots");
   return eb;
 }
@@ -868,8 +891,12 @@ struct VerifyResult {
   }
 };
 
+// cast (optional, one flag per ballot, 0 = spoiled): every ballot is verified, only the cast ones
+// are tallied; spoiled ballots go to Decryption::decryptBallots (RunRemoteDecryptor.java:264-269)
 inline VerifyResult verifyBallots(const GroupContext& G, const ElementModP& K, const ElementModQ& qbar,
-                                  const Manifest& man, const EncryptedBallots& eb) {
+                                  const Manifest& man, const EncryptedBallots& eb,
+                                  const std::vector<uint8_t>* cast = nullptr) {
+  if (cast && cast->size() != eb.n) throw std::invalid_argument("verifyBallots: one cast flag per ballot");
   VerifyResult r;
   r.okSelection.assign(eb.n * man.nsel(), 0);
   r.okContest.assign(eb.n * man.nContests, 0);
@@ -877,11 +904,36 @@ inline VerifyResult verifyBallots(const GroupContext& G, const ElementModP& K, c
   const auto qb = qbar.byteArray();
   check(eg_verify_ballots(G.handle(), K.byteArray(), qb.data(), eb.n, man.nContests, man.spc(), man.votesAllowed,
                           (uint32_t)man.votesAllowed, eb.cts.data(), eb.rproof.data(), eb.cproof.data(),
-                          r.okSelection.data(), r.okContest.data(), tal.data()),
+                          cast ? cast->data() : nullptr, r.okSelection.data(), r.okContest.data(), tal.data()),
         "eg_verify_ballots");
   for (size_t i = 0; i < man.nReal(); ++i)
     r.tally.push_back({ElementModP(&tal[(2 * i) * EG_P_BYTES], &G), ElementModP(&tal[(2 * i + 1) * EG_P_BYTES], &G)});
   return r;
+}
+
+// Decryption.decryptBallot (RunRemoteDecryptor.java:264-269) over a batch of spoiled ballots:
+// every ballot's real selections (placeholders are not part of the plaintext) go to the trustees
+// as ONE batch per guardian, then the same share checks, Lagrange combine and dLog (<= votes
+// allowed) as the tally.  -> per ballot, its decrypted selections (nullopt: not a valid count).
+inline std::vector<std::vector<std::optional<int64_t>>> decryptBallots(Decryption& dec, const Manifest& man,
+                                                                        const EncryptedBallots& spoiled,
+                                                                        const GroupContext& G,
+                                                                        DecryptionRecord* record = nullptr) {
+  std::vector<ElGamalCiphertext> texts;
+  texts.reserve(spoiled.n * man.nReal());
+  for (size_t b = 0; b < spoiled.n; ++b)
+    for (size_t c = 0; c < man.nContests; ++c)
+      for (size_t s = 0; s < man.nSelections; ++s) {
+        const uint8_t* ct = &spoiled.cts[((b * man.nsel()) + c * man.spc() + s) * 2 * EG_P_BYTES];
+        texts.push_back({ElementModP(ct, &G), ElementModP(ct + EG_P_BYTES, &G)});
+      }
+  std::vector<std::vector<std::optional<int64_t>>> out(spoiled.n);
+  if (texts.empty()) return out;
+  DecryptionRecord rec = dec.decryptRecord(texts, (int64_t)man.votesAllowed);
+  for (size_t b = 0; b < spoiled.n; ++b)
+    out[b].assign(rec.counts.begin() + b * man.nReal(), rec.counts.begin() + (b + 1) * man.nReal());
+  if (record) *record = std::move(rec);
+  return out;
 }
 
 }  // namespace electionguard

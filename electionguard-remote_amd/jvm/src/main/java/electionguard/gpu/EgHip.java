@@ -37,8 +37,15 @@ public final class EgHip {
 
   public static native void profileBegin(long ctx);
 
-  /** @return {kernel ms, Montgomery ops, of which squarings, launches, shader clock GHz} of the dominant kernel. */
+  /**
+   * @return {kernel ms, Montgomery ops, of which squarings, launches, shader clock GHz (median per
+   *     workgroup; 0 if no record was usable), clock records used, clock records dropped} of the
+   *     dominant kernel.
+   */
   public static native double[] profileEnd(long ctx);
+
+  /** eg_clock_median over (shader ticks, 100 MHz real-time ticks) pairs: {GHz, used, dropped}. */
+  public static native double[] clockMedian(long[] recs);
 
   /** The fixed-base table of g built at ctxCreate (owned by the context: do not destroy). */
   public static native long gTable(long ctx);
@@ -72,23 +79,27 @@ public final class EgHip {
 
   // ---- ballots: Verifier(record, 11).verify() + runAccumulateBallots, batchEncryption ----
   // (RunRemoteWorkflowTest.java:140-141,151,179-182).  Layouts: include/eg_hip.h.
+  /** cast: one byte per ballot (0 = spoiled: verified, not tallied), or null for all cast. */
   public static native void verifyBallots(long ctx, byte[] K512, byte[] qbar32, int nb, int nc, int spc,
                                           int placeholders, int limit, byte[] cts, byte[] rproof, byte[] cproof,
-                                          byte[] okSel, byte[] okContest, byte[] tally);
+                                          byte[] cast, byte[] okSel, byte[] okContest, byte[] tally);
 
   public static native void setElectionKey(long ctx, byte[] K512, int windowBits);
 
-  public static native void verifyBallotsDev(long ctx, byte[] qbar32, long nb, long nc, long spc, long placeholders,
-                                             int limit, long dCts, long dRproof, long dCproof, long dOkSel,
-                                             long dOkContest, long dTally);
+  public static native void verifyBallotsDev(long ctx, byte[] K512, byte[] qbar32, long nb, long nc, long spc,
+                                             long placeholders, int limit, long dCts, long dRproof, long dCproof,
+                                             long dCast, long dOkSel, long dOkContest, long dTally);
 
-  public static native void encryptBallots(long ctx, byte[] qbar32, int nb, int nc, int spc, byte[] votes,
+  public static native void encryptBallots(long ctx, byte[] K512, byte[] qbar32, int nb, int nc, int spc, byte[] votes,
                                            byte[] selNonces, byte[] contestNonces, byte[] cts, byte[] rproof,
                                            byte[] cproof);
 
-  public static native void encryptBallotsDev(long ctx, byte[] qbar32, long nb, long nc, long spc, long dVotes,
-                                              long dSelNonces, long dContestNonces, long dCts, long dRproof,
-                                              long dCproof);
+  public static native void encryptBallotsDev(long ctx, byte[] K512, byte[] qbar32, long nb, long nc, long spc,
+                                              long dVotes, long dSelNonces, long dContestNonces, long dCts,
+                                              long dRproof, long dCproof);
+
+  /** Constant-time encryption (masked scans of small tables; eg_ctx_set_ct_encrypt). */
+  public static native void setCtEncrypt(long ctx, boolean on);
 
   // ---- trustee (DecryptingTrusteeIF, RunRemoteDecryptingTrustee.java:189-193,227-232) ----
   public static native void trusteeDecryptBatch(long ctx, byte[] secret32, byte[] qbar32, byte[] texts, byte[] nonces,
@@ -97,4 +108,24 @@ public final class EgHip {
   /** Mediator side of Decryption.decrypt (RunRemoteDecryptor.java:261-262): share-proof checks. */
   public static native void verifyShares(long ctx, byte[] qbar32, byte[] Ki, byte[] texts, byte[] M, byte[] proof,
                                          int n, byte[] ok);
+
+  // ---- per-element calls, coalesced across threads into GPU batches (eg_powp_one & co.) ----
+  // The upstream pattern: ElementModP.powP / times, GroupContext.gPowP one element per call from
+  // 11 threads (RunRemoteWorkflowTest.java:140,180).
+  public static native void setCoalescing(long ctx, long maxBatch, int windowUs);
+
+  public static native void powpOne(long ctx, byte[] base512, byte[] exp32, byte[] out512);
+
+  public static native void gpowpOne(long ctx, byte[] exp32, byte[] out512);
+
+  public static native void multpOne(long ctx, byte[] a512, byte[] b512, byte[] out512);
+
+  /** Asynchronous forms: a handle to pass to {@link #ticketWait} exactly once. */
+  public static native long powpSubmit(long ctx, byte[] base512, byte[] exp32);
+
+  public static native long gpowpSubmit(long ctx, byte[] exp32);
+
+  public static native long multpSubmit(long ctx, byte[] a512, byte[] b512);
+
+  public static native void ticketWait(long ticket, byte[] out512);
 }

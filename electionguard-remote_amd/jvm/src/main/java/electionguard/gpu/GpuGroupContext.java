@@ -170,6 +170,53 @@ public final class GpuGroupContext implements AutoCloseable {
     return unpackP(out, n);
   }
 
+  // ------------------------------------------------------------------ per-element (coalesced)
+  // The upstream API's call pattern: one element per call, from many threads.  Concurrent calls
+  // join one GPU batch inside the library (eg_powp_one / eg_gpowp_one / eg_multp_one); a thread
+  // that has several independent elements submits them all first (powPAsync) and then waits.
+
+  /** base.powP(e) (ElementModP.powP, variable base). */
+  public ElementModP powP(ElementModP base, ElementModQ e) {
+    byte[] b = new byte[EgHip.P_BYTES], x = new byte[EgHip.Q_BYTES], out = new byte[EgHip.P_BYTES];
+    put(b, 0, base.byteArray(), EgHip.P_BYTES);
+    put(x, 0, e.byteArray(), EgHip.Q_BYTES);
+    EgHip.powpOne(ctx, b, x, out);
+    return elementP(out, 0);
+  }
+
+  /** g^e (GroupContext.gPowP). */
+  public ElementModP gPowP(ElementModQ e) {
+    byte[] x = new byte[EgHip.Q_BYTES], out = new byte[EgHip.P_BYTES];
+    put(x, 0, e.byteArray(), EgHip.Q_BYTES);
+    EgHip.gpowpOne(ctx, x, out);
+    return elementP(out, 0);
+  }
+
+  /** a.times(b). */
+  public ElementModP multP(ElementModP a, ElementModP b) {
+    byte[] x = new byte[EgHip.P_BYTES], y = new byte[EgHip.P_BYTES], out = new byte[EgHip.P_BYTES];
+    put(x, 0, a.byteArray(), EgHip.P_BYTES);
+    put(y, 0, b.byteArray(), EgHip.P_BYTES);
+    EgHip.multpOne(ctx, x, y, out);
+    return elementP(out, 0);
+  }
+
+  /** base.powP(e) queued now, completed by the library's next batch. */
+  public java.util.concurrent.CompletableFuture<ElementModP> powPAsync(ElementModP base, ElementModQ e) {
+    byte[] b = new byte[EgHip.P_BYTES], x = new byte[EgHip.Q_BYTES];
+    put(b, 0, base.byteArray(), EgHip.P_BYTES);
+    put(x, 0, e.byteArray(), EgHip.Q_BYTES);
+    final long t = EgHip.powpSubmit(ctx, b, x);
+    return java.util.concurrent.CompletableFuture.supplyAsync(() -> {
+      byte[] out = new byte[EgHip.P_BYTES];
+      EgHip.ticketWait(t, out);
+      return elementP(out, 0);
+    });
+  }
+
+  /** Batch window of the per-element calls (defaults: 16384 elements, 100 us). */
+  public void setCoalescing(long maxBatch, int windowUs) { EgHip.setCoalescing(ctx, maxBatch, windowUs); }
+
   // ------------------------------------------------------------------ ballots
 
   /** Verdicts and tally of {@link #verifyBallots}. */
@@ -194,13 +241,24 @@ public final class GpuGroupContext implements AutoCloseable {
   public BallotVerification verifyBallots(ElementModP jointKey, ElementModQ qbar, int nb, int ncontests, int spc,
                                           int placeholders, int limit, byte[] cts, byte[] rproof, byte[] cproof,
                                           boolean withTally) {
+    return verifyBallots(jointKey, qbar, nb, ncontests, spc, placeholders, limit, cts, rproof, cproof, null, withTally);
+  }
+
+  /**
+   * Same, with a cast flag per ballot (0 = spoiled: verified but not tallied; the spoiled ballots
+   * are decrypted one by one, RunRemoteDecryptor.java:264-269), or null for all cast.
+   */
+  public BallotVerification verifyBallots(ElementModP jointKey, ElementModQ qbar, int nb, int ncontests, int spc,
+                                          int placeholders, int limit, byte[] cts, byte[] rproof, byte[] cproof,
+                                          byte[] cast, boolean withTally) {
     byte[] k = new byte[EgHip.P_BYTES], qb = new byte[EgHip.Q_BYTES];
     put(k, 0, jointKey.byteArray(), EgHip.P_BYTES);
     put(qb, 0, qbar.byteArray(), EgHip.Q_BYTES);
     final int nsel = ncontests * spc;
     byte[] okS = new byte[nb * nsel], okC = new byte[nb * ncontests];
     byte[] tally = withTally ? new byte[ncontests * (spc - placeholders) * 2 * EgHip.P_BYTES] : null;
-    EgHip.verifyBallots(ctx, k, qb, nb, ncontests, spc, placeholders, limit, cts, rproof, cproof, okS, okC, tally);
+    EgHip.verifyBallots(ctx, k, qb, nb, ncontests, spc, placeholders, limit, cts, rproof, cproof, cast, okS, okC,
+        tally);
     return new BallotVerification(okS, okC, tally);
   }
 
@@ -213,7 +271,7 @@ public final class GpuGroupContext implements AutoCloseable {
     EgHip.setElectionKey(ctx, k, keyWindowBits);
     final int nsel = ncontests * spc;
     byte[] cts = new byte[nb * nsel * 1024], rp = new byte[nb * nsel * 128], cp = new byte[nb * ncontests * 64];
-    EgHip.encryptBallots(ctx, qb, nb, ncontests, spc, votes, selNonces, contestNonces, cts, rp, cp);
+    EgHip.encryptBallots(ctx, k, qb, nb, ncontests, spc, votes, selNonces, contestNonces, cts, rp, cp);
     return new byte[][] {cts, rp, cp};
   }
 }

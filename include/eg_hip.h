@@ -76,10 +76,15 @@ int eg_ctx_sync(eg_ctx* ctx);
  * Any out pointer may be NULL. */
 int eg_ctx_profile_begin(eg_ctx* ctx);
 int eg_ctx_profile_end(eg_ctx* ctx, double* kernel_ms, double* mont_ops, double* squarings, int* launches);
-/* Shader clock (GHz) the k_pow launches of the last profile_begin/end window ran at: each
- * workgroup's clock64() cycles over its wall_clock64() ticks, summed over workgroups
- * (0 when nothing was profiled).  Instrumentation; no reference counterpart. */
-int eg_ctx_profile_clock(eg_ctx* ctx, double* ghz);
+/* Shader clock (GHz) the k_pow launches of the last profile_begin/end window ran at: the median
+ * over workgroups of (s_memtime ticks / s_memrealtime ticks) x 100 MHz (eg_clock_median), with
+ * the number of clock records used and dropped (unset, wrapped or out of range).  0 GHz when no
+ * record was usable.  used / dropped may be NULL.  Instrumentation; no reference counterpart. */
+int eg_ctx_profile_clock(eg_ctx* ctx, double* ghz, uint32_t* used, uint32_t* dropped);
+/* The reduction behind it, a pure host function: recs = n pairs (shader ticks, 100 MHz real-time
+ * ticks).  A record is dropped when a field is 0 or >= 2^62 (unset / wrapped), the real-time span
+ * is under 10 us, or its ratio lies outside [0.5, 3.5] GHz; *ghz = median of the rest, or 0. */
+int eg_clock_median(const uint64_t* recs, size_t n, double* ghz, uint32_t* used, uint32_t* dropped);
 /* Fixed-base table for g (built at ctx creation) — accessor. */
 eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
 
@@ -132,34 +137,49 @@ int eg_multinv_batch(eg_ctx* ctx, const uint8_t* a_be, uint8_t* out_be, size_t n
  * Selections are contest-major; contest k owns selections [k*spc, (k+1)*spc)
  * (placeholders last: the tally skips the last `placeholders` of each contest).
  * K_be = joint election key, qbar_be = extended base hash, limit = votesAllowed.
+ * cast (may be NULL = every ballot cast): nballots bytes, 0 = spoiled.  Every ballot is
+ * verified; only cast ballots enter the tally (runAccumulateBallots sums cast ballots, the
+ * spoiled ones are decrypted individually, RunRemoteDecryptor.java:264-269).
  * Outputs: ok_sel[nballots*nsel], ok_contest[nballots*ncontest] (1 = valid),
- * tally_be[ncontest*(spc-placeholders)*2*512] (may be NULL). */
+ * tally_be[ncontest*(spc-placeholders)*2*512] (may be NULL; all ones for no cast ballot).
+ * The key is set under the ctx lock for the call (a matching table is reused; a different K
+ * rebuilds it at the window width of the ctx's current table, see eg_set_election_key). */
 int eg_verify_ballots(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], const uint8_t qbar_be[EG_Q_BYTES],
                       size_t nballots, size_t ncontest, size_t spc, size_t placeholders,
                       uint32_t limit, const uint8_t* cts, const uint8_t* rproof,
-                      const uint8_t* cproof, uint8_t* ok_sel, uint8_t* ok_contest,
+                      const uint8_t* cproof, const uint8_t* cast, uint8_t* ok_sel, uint8_t* ok_contest,
                       uint8_t* tally_be);
-/* Same, device pointers, asynchronous on the ctx stream.  K must be registered
- * first with eg_set_election_key (builds its fixed-base table once). */
+/* Builds K's fixed-base radix table (window_bits in [4, 22]; g's table follows the width) once,
+ * so later calls with the same K only compare it. */
 int eg_set_election_key(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], int window_bits);
-int eg_verify_ballots_dev(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nballots,
-                          size_t ncontest, size_t spc, size_t placeholders, uint32_t limit,
+/* Same as eg_verify_ballots, device pointers (d_cast may be NULL), asynchronous on the ctx stream. */
+int eg_verify_ballots_dev(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], const uint8_t qbar_be[EG_Q_BYTES],
+                          size_t nballots, size_t ncontest, size_t spc, size_t placeholders, uint32_t limit,
                           const uint8_t* d_cts, const uint8_t* d_rproof, const uint8_t* d_cproof,
-                          uint8_t* d_ok_sel, uint8_t* d_ok_contest, uint8_t* d_tally_be);
+                          const uint8_t* d_cast, uint8_t* d_ok_sel, uint8_t* d_ok_contest,
+                          uint8_t* d_tally_be);
 
 /* ---- batched encryption (batchEncryption, RunRemoteWorkflowTest.java:140-141) ----
  * Per selection: plaintext m (0/1), nonces (R, u, c_fake, v_fake) as 4*32 B.
  * Per contest: constant-proof nonce u (32 B).  Outputs cts / rproof / cproof in
- * the eg_verify_ballots layout.  Requires eg_set_election_key. */
-int eg_encrypt_ballots(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nballots,
-                       size_t ncontest, size_t spc, const uint8_t* votes,
+ * the eg_verify_ballots layout.  K_be is set for the call as in eg_verify_ballots. */
+int eg_encrypt_ballots(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], const uint8_t qbar_be[EG_Q_BYTES],
+                       size_t nballots, size_t ncontest, size_t spc, const uint8_t* votes,
                        const uint8_t* sel_nonces, const uint8_t* contest_nonces,
                        uint8_t* cts, uint8_t* rproof, uint8_t* cproof);
+/* Constant-time encryption (on != 0): the fixed-base terms of eg_encrypt_ballots[_dev] read the
+ * 6-bit radix tables of g and K (1.76 MB each, built once per key) with masked scans of every
+ * window's 64 entries instead of indexing 22-bit tables by nonce digits, so neither the schedule
+ * nor any address depends on a nonce or a vote (the commitments of both proof branches are
+ * computed and put in order with masks in either mode).  The bytes are identical; the rate is
+ * lower.  The trustee's kernels are always constant-time. */
+int eg_ctx_set_ct_encrypt(eg_ctx* ctx, int on);
 /* Same, device pointers (inputs and outputs resident in HBM); returns when the outputs
  * are written.  The votes (1 byte per selection) are read back to the host to build the
- * job tables; nonces and outputs never leave the device. */
-int eg_encrypt_ballots_dev(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], size_t nballots,
-                           size_t ncontest, size_t spc, const uint8_t* d_votes,
+ * job tables (except in constant-time mode, eg_ctx_set_ct_encrypt); nonces and outputs never
+ * leave the device. */
+int eg_encrypt_ballots_dev(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], const uint8_t qbar_be[EG_Q_BYTES],
+                           size_t nballots, size_t ncontest, size_t spc, const uint8_t* d_votes,
                            const uint8_t* d_sel_nonces, const uint8_t* d_contest_nonces,
                            uint8_t* d_cts, uint8_t* d_rproof, uint8_t* d_cproof);
 
@@ -177,6 +197,30 @@ int eg_trustee_decrypt_batch(eg_ctx* ctx, const uint8_t secret_be[EG_Q_BYTES],
 int eg_verify_shares(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], const uint8_t* Ki_be,
                      const uint8_t* texts, const uint8_t* M_be, const uint8_t* proof, size_t n,
                      uint8_t* ok);
+
+/* ---- per-element calls, coalesced (upstream ElementModP.powP / times, GroupContext.gPowP,
+ * called element by element from 11 threads: RunRemoteWorkflowTest.java:140,180, on the group
+ * of KUtils.java:10-12) ----
+ * eg_*_submit queues one element on the ctx's open batch of its kind and returns a ticket at
+ * once; a dispatcher thread runs the batch as one eg_powp_batch / eg_fb_pow_batch (g) /
+ * eg_multp_batch once the GPU is free and the oldest element has waited window_us, or when
+ * max_batch elements are queued.  The caller's out must stay valid until eg_ticket_wait, which
+ * blocks until the result is in out, frees the ticket and returns the batch's status.  Wait for
+ * every ticket before eg_ctx_destroy (destroy first runs the queued elements).
+ * eg_*_one = submit + wait.  Defaults: max_batch 16384, window 100 us. */
+typedef struct eg_ticket eg_ticket;
+int eg_ctx_set_coalescing(eg_ctx* ctx, size_t max_batch, uint32_t window_us);
+int eg_powp_submit(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], const uint8_t exp_be[EG_Q_BYTES],
+                   uint8_t out_be[EG_P_BYTES], eg_ticket** ticket);
+int eg_gpowp_submit(eg_ctx* ctx, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES], eg_ticket** ticket);
+int eg_multp_submit(eg_ctx* ctx, const uint8_t a_be[EG_P_BYTES], const uint8_t b_be[EG_P_BYTES],
+                    uint8_t out_be[EG_P_BYTES], eg_ticket** ticket);
+int eg_ticket_wait(eg_ticket* ticket);
+int eg_powp_one(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], const uint8_t exp_be[EG_Q_BYTES],
+                uint8_t out_be[EG_P_BYTES]);
+int eg_gpowp_one(eg_ctx* ctx, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES]);
+int eg_multp_one(eg_ctx* ctx, const uint8_t a_be[EG_P_BYTES], const uint8_t b_be[EG_P_BYTES],
+                 uint8_t out_be[EG_P_BYTES]);
 
 #ifdef __cplusplus
 }

@@ -371,10 +371,14 @@ def verify_ballot(G: Group, K: int, qbar: int, man: Manifest, eb: EncryptedBallo
     return ok
 
 
-def accumulate_tally(G: Group, man: Manifest, ballots: Sequence[EncryptedBallot]) -> List[Ciphertext]:
+def accumulate_tally(G: Group, man: Manifest, ballots: Sequence[EncryptedBallot],
+                     cast: Optional[Sequence[bool]] = None) -> List[Ciphertext]:
     """runAccumulateBallots (RunRemoteWorkflowTest.java:151): per real selection,
-    componentwise product of ciphertexts over cast ballots; placeholders excluded."""
+    componentwise product of ciphertexts over CAST ballots (cast[i] false = spoiled, left to
+    decryptBallot, RunRemoteDecryptor.java:264-269); placeholders excluded."""
     spc = man.sel_per_contest
+    if cast is not None:
+        ballots = [b for b, c in zip(ballots, cast) if c]
     out = []
     for c in range(man.n_contests):
         for s in range(man.n_selections):
@@ -548,3 +552,27 @@ def combine(G: Group, ct: Ciphertext, direct: Dict[str, int], comp: Dict[str, Di
             M = G.multP(M, G.powP(Mli, lagrange(xs, avail_x[gid], G.q)))
     T = G.multP(ct.data, G.multInv(M))
     return G.dlogG(T, max_t)
+
+
+def decrypt_ballot(G: Group, qbar: int, man: Manifest, eb: EncryptedBallot, avail: Sequence[Guardian],
+                   missing: Sequence[Guardian], nonces: Sequence[int]) -> Tuple[List[Optional[int]], dict]:
+    """decryptBallot of one spoiled ballot (RunRemoteDecryptor.java:264-269): each real
+    selection (placeholders are not part of the plaintext ballot) is decrypted like a tally
+    text -- every available guardian's direct share, every (missing, available) pair's
+    compensated share, Lagrange combine, dLog_g up to votesAllowed.  nonces: the proof nonces,
+    one per (share kind, text) in the order direct(avail...) then compensated(missing x avail),
+    each list len(texts) long.  -> (plaintexts, shares by kind)."""
+    spc = man.sel_per_contest
+    texts = [eb.cts[c * spc + s] for c in range(man.n_contests) for s in range(man.n_selections)]
+    n = len(texts)
+    it = iter(nonces)
+    take = lambda: [next(it) for _ in range(n)]  # noqa: E731
+    direct = {g.gid: direct_decrypt(G, qbar, g, texts, take()) for g in avail}
+    comp = {l.gid: {g.gid: compensated_decrypt(G, qbar, g, l, texts, take()) for g in avail} for l in missing}
+    avail_x = {g.gid: g.x for g in avail}
+    out = []
+    for i, ct in enumerate(texts):
+        out.append(combine(G, ct, {gid: d[i][0] for gid, d in direct.items()},
+                           {l: {gid: c[i][0] for gid, c in by.items()} for l, by in comp.items()},
+                           avail_x, man.votes_allowed))
+    return out, {"direct": direct, "compensated": comp}

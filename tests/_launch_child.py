@@ -38,6 +38,13 @@ def fold(elems, groups, length):
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
+    fail = os.environ.get("EG_TEST_FAIL_RANK")  # "r:code": rank r exits with code, the others wait for it
+    if fail:
+        r, code = (int(x) for x in fail.split(":"))
+        if rank == r:
+            os._exit(code)
+        dist.barrier()  # blocks: the failed rank never arrives (the launcher must end this)
+        return
     G = O.production_group()
     nb, n_real = 5, 2
     cts = ballots(nb, n_real)

@@ -96,6 +96,46 @@ def trustee(G):
     }
 
 
+def spoiled(G):
+    """Cast / spoiled ballots (RunRemoteDecryptor.java:264-269): 5 guardians, quorum 3, guardians
+    4 and 5 missing; 4 ballots of which 1 and 3 are spoiled.  The tally covers the cast ballots
+    only; each spoiled ballot is decrypted selection by selection with injected proof nonces."""
+    rng = random.Random(404)
+    gs, K = O.key_ceremony(G, 5, 3, rng)
+    qbar = rng.randrange(G.q)
+    man = O.Manifest(2, 3, 1)
+    cast = [True, False, True, False]
+    ebs, votes_all = [], []
+    for _ in cast:
+        votes = O.ballot_plaintexts(man, rng)
+        votes_all.append(votes)
+        ebs.append(O.encrypt_ballot(G, K, qbar, man, votes, rng))
+    tally = O.accumulate_tally(G, man, ebs, cast)
+    avail, missing = gs[:3], gs[3:]
+    n_real = man.n_contests * man.n_selections
+    out = {"K": hx(K, 512), "qbar": hx(qbar, 32), "manifest": [2, 3, 1], "cast": cast,
+           "guardians": [{"x": g.x, "coeffs": [hx(a, 32) for a in g.coeffs],
+                          "commitments": [hx(k, 512) for k in g.commitments]} for g in gs],
+           "available": [g.gid for g in avail], "missing": [g.gid for g in missing],
+           "ballots": [], "tally": [[hx(ct.pad, 512), hx(ct.data, 512)] for ct in tally]}
+    for eb, votes, c in zip(ebs, votes_all, cast):
+        b = {"votes": votes, "cts": [[hx(ct.pad, 512), hx(ct.data, 512)] for ct in eb.cts],
+             "rproofs": [[hx(v, 32) for v in (pr.c0, pr.v0, pr.c1, pr.v1)] for pr in eb.proofs],
+             "cproofs": [[hx(pr.c, 32), hx(pr.v, 32)] for pr in eb.contest_proofs]}
+        if not c:
+            nonces = [rng.randrange(1, G.q) for _ in range(n_real * (len(avail) + len(avail) * len(missing)))]
+            plain, shares = O.decrypt_ballot(G, qbar, man, eb, avail, missing, nonces)
+            b["nonces"] = [hx(u, 32) for u in nonces]
+            b["plaintext"] = plain
+            b["direct"] = {gid: [{"M": hx(M, 512), "c": hx(p.c, 32), "v": hx(p.v, 32)} for M, p in d]
+                           for gid, d in shares["direct"].items()}
+            b["compensated"] = {l: {gid: [{"M": hx(M, 512), "c": hx(p.c, 32), "v": hx(p.v, 32), "recovery": hx(rk, 512)}
+                                          for M, p, rk in d] for gid, d in by.items()}
+                                for l, by in shares["compensated"].items()}
+        out["ballots"].append(b)
+    return out
+
+
 if __name__ == "__main__":
     for mode in (O.MODE4096, O.MODE4096_V2):
         out = HERE / mode
@@ -104,6 +144,7 @@ if __name__ == "__main__":
         (out / "group_ops.json").write_text(json.dumps(group_ops(G), indent=0))
         (out / "ballots.json").write_text(json.dumps(ballots(G), indent=0))
         (out / "trustee.json").write_text(json.dumps(trustee(G), indent=0))
+        (out / "spoiled.json").write_text(json.dumps(spoiled(G), indent=0))
         p, q, g, r = O.derive_group(mode)
         (out / "constants.json").write_text(json.dumps({"mode": mode, "p": hx(p, 512), "q": hx(q, 32),
                                                         "g": hx(g, 512), "r": hx(r, 512)}, indent=0))

@@ -126,3 +126,34 @@ def test_bench_config_names():
     assert config_name(4, 5, 10_000, 8) == "configs[1] shape (4x5), 10000 ballots per GPU x 8 GPUs"
     assert config_name(4, 5, 2_000, 2).startswith("configs[1] shape")
     assert config_name(20, 5, 10_000, 4).startswith("configs[4] shape")
+    assert config_name(20, 5, 250_000, 4).startswith("configs[4] (1M ballots")
+
+
+def test_bench_default_workload_per_gpu_count():
+    """N = 1 measures configs[1] (10k ballots); N > 1 measures configs[2] (1M ballots over the
+    node, 1M // N per rank), without any flag."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from bench import config_name, default_ballots
+    assert default_ballots(1) == 10_000 and config_name(4, 5, default_ballots(1), 1) == "configs[1]"
+    for n in (2, 4, 8):
+        assert default_ballots(n) * n == 1_000_000
+        assert config_name(4, 5, default_ballots(n), n) == f"configs[2] (1M ballots over {n} GPUs)"
+
+
+def test_launcher_fails_fast_when_a_rank_dies(tmp_path):
+    """run_ranks (bench.py's self-launch) polls every rank: rank 1 exits 3 while rank 0 waits in
+    a collective for it, and the launcher returns 3 within seconds (killing rank 0) instead of
+    waiting for the collective's timeout."""
+    import sys
+    import time
+    from pathlib import Path
+    from electionguard.launch import run_ranks
+    child = Path(__file__).resolve().parent / "_launch_child.py"
+    env = dict(os.environ, EG_TEST_FAIL_RANK="1:3")
+    env.pop("WORLD_SIZE", None)
+    t = time.monotonic()
+    rc = run_ranks(str(child), [str(tmp_path / "unused.json")], 2, timeout=240, env=env)
+    assert rc == 3
+    assert time.monotonic() - t < 60

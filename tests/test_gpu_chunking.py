@@ -244,9 +244,9 @@ def test_oversized_arguments_rejected(group):
     assert rc == 1
     rc = lib.eg_prod_reduce(group.handle, one, 1 << 16, 1 << 16, one)
     assert rc == 1
-    rc = lib.eg_verify_ballots_dev(group.handle, one, 1, 1 << 21, 1, 0, 1, one, one, one, one, one, None)
+    rc = lib.eg_verify_ballots_dev(group.handle, one, one, 1, 1 << 21, 1, 0, 1, one, one, one, None, one, one, None)
     assert rc == 1 and b"manifest" in lib.eg_last_error()
-    rc = lib.eg_encrypt_ballots(group.handle, one, 1, 1 << 11, 1 << 10, one, one, one, one, one, one)
+    rc = lib.eg_encrypt_ballots(group.handle, one, one, 1, 1 << 11, 1 << 10, one, one, one, one, one, one)
     assert rc == 1 and b"manifest" in lib.eg_last_error()
 
 

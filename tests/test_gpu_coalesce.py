@@ -1,0 +1,83 @@
+"""GPU: per-element calls coalesced behind the C ABI (eg_powp_one / eg_multp_one / eg_gpowp_one and
+eg_powp_submit + eg_ticket_wait).  The reference drives the group one element per call from 11
+threads (RunRemoteWorkflowTest.java:140,180) on the context KUtils.productionGroup() makes
+(KUtils.java:10-12); concurrent calls must join GPU batches and stay bit-exact.
+
+* the C++ driver (tests/cpp/coalesce_bench.cpp, built in-tree by __graft_entry__.build()) runs 11
+  threads of per-element calls on vectors whose expected results come from CPython pow (the
+  oracle) and reports their rates beside one eg_powp_batch call;
+* 11 Python threads through ElementModP.powP / times and GroupContext.gPowP (the ctypes mirror),
+  checked against CPython pow."""
+import json
+import random
+import struct
+import subprocess
+import threading
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+BIN = ROOT / "electionguard-remote_amd" / "host" / "_build" / "coalesce_bench"
+
+
+def test_cpp_eleven_threads_per_element_bitexact(group, tmp_path):
+    import eg_oracle as O
+    og = O.production_group()
+    rng = random.Random(17)
+    n = 1500
+    recs = []
+    for i in range(n):
+        b = rng.randrange(og.p) if i % 7 else rng.choice([0, 1, og.p - 1, og.p, 2**4096 - 1])
+        e = rng.randrange(og.q) if i % 11 else rng.choice([0, 1, og.q - 1, 2**256 - 1])
+        b2 = rng.randrange(2**4096)
+        recs.append(b.to_bytes(512, "big") + e.to_bytes(32, "big") + pow(b, e, og.p).to_bytes(512, "big") +
+                    b2.to_bytes(512, "big") + (b * b2 % og.p).to_bytes(512, "big") +
+                    pow(og.g, e, og.p).to_bytes(512, "big"))
+    vec = tmp_path / "vectors.bin"
+    vec.write_bytes(struct.pack("<I", n) + b"".join(recs))
+    assert BIN.exists(), "run __graft_entry__.build() first"
+    r = subprocess.run([str(BIN), str(vec), "11"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(res)
+    assert res["mismatches"] == 0 and res["threads"] == 11
+    # submit-all-then-wait forms full batches: within reach of the one batch call
+    assert res["powp_submit_wait_per_s"] > 0.25 * res["powp_batch_per_s"]
+
+
+def test_python_threads_per_element_bitexact(group):
+    from electionguard.core.group import ElementModP, ElementModQ
+    rng = random.Random(23)
+    p, q, g = group.p, group.q, group.g
+    work = [(rng.randrange(p), rng.randrange(q), rng.randrange(p)) for _ in range(11 * 12)]
+    bad = []
+
+    def run(k):
+        for i in range(k, len(work), 11):
+            b, e, c = work[i]
+            x = ElementModP(b, group)
+            if x.powP(ElementModQ(e, group)).value != pow(b, e, p):
+                bad.append(("powP", i))
+            if x.times(ElementModP(c, group)).value != b * c % p:
+                bad.append(("times", i))
+            if group.gPowP(e).value != pow(g, e, p):
+                bad.append(("gPowP", i))
+
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(11)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not bad, bad[:5]
+
+
+def test_coalescing_window_and_errors(group):
+    from electionguard.core import native
+    group.set_coalescing(4, 50)
+    out = group.powP_one(3, 5)
+    assert int.from_bytes(out, "big") == 243
+    group.set_coalescing(16384, 100)
+    with pytest.raises(native.EgError):
+        group.set_coalescing(0, 100)

@@ -94,3 +94,55 @@ def test_concurrent_verifiers_one_context(group):
     for k in range(2):
         s, c, _ = got[("bad", k)]
         assert not s[2, 4] and s.sum() == s.size - 1 and c.all()
+
+
+def test_two_keys_on_one_context_device_paths(group):
+    """Threads using DIFFERENT election keys on the one shared context (productionGroup): every
+    device-pointer verify and encryption call passes its own K and the library sets it under the
+    ctx lock for that call, so no call can run against another thread's key (the
+    ensure()-then-call sequence used to race).  Each thread encrypts on the device, checks the
+    bytes against its own host encryption made before the threads start, and verifies on the
+    device; a tally under the wrong key would fail the proofs."""
+    import numpy as np
+    import torch
+    from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption, batch_encryption_device,
+                                      random_scalars, random_votes)
+    from electionguard.keyceremony import key_ceremony
+    man = Manifest(2, 3, 1)
+    dev = torch.device("cuda", 0)
+    jobs = []
+    for seed in (101, 202, 303):
+        _, K = key_ceremony(group, 2, 2, seed=seed)
+        key = ElectionKey(group, K)
+        rng = np.random.default_rng(seed)
+        nb = 40
+        votes = random_votes(rng, man, nb)
+        sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
+        cn = random_scalars(rng, (nb, man.n_contests), group.q)
+        ref = batch_encryption(group, key, seed, man, votes, sn, cn)
+        jobs.append((seed, key, nb, votes, sn, cn, ref))
+    torch.cuda.synchronize()
+    ok = {}
+
+    def run(seed, key, nb, votes, sn, cn, ref):
+        def f():
+            dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (votes, sn, cn))
+            oc = torch.empty(ref.cts.shape, dtype=torch.uint8, device=dev)
+            orp = torch.empty(ref.rproof.shape, dtype=torch.uint8, device=dev)
+            ocp = torch.empty(ref.cproof.shape, dtype=torch.uint8, device=dev)
+            oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
+            okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            V = Verifier(group, key, seed, man)
+            res = []
+            for _ in range(4):
+                batch_encryption_device(group, key, seed, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
+                                        oc.data_ptr(), orp.data_ptr(), ocp.data_ptr())
+                V.verify_device(oc.data_ptr(), orp.data_ptr(), ocp.data_ptr(), nb, oks.data_ptr(), okc.data_ptr(), None)
+                group.sync()
+                res.append(bool(np.array_equal(oc.cpu().numpy(), ref.cts)) and bool(oks.all()) and bool(okc.all()))
+            ok[seed] = res
+        return f
+
+    _run_threads([run(*j) for j in jobs])
+    assert ok == {s: [True] * 4 for s, *_ in jobs}, ok

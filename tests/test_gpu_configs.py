@@ -6,7 +6,10 @@ size-independent properties (the CPU oracle cannot redo them in a test's time):
   valid; the tally decrypts (joint secret, BSGS dLog) to exactly the per-selection vote sums;
   and the two-rank fold (each half verified alone, partial tallies multiplied mod p as
   electionguard.distributed.gather_fold_tally does on rank 0) equals the single tally.
-* configs[4] -- the 100-selection manifest (20 x 5): 10,000 ballots, same checks.
+* configs[4] -- the 100-selection manifest (20 x 5): 10,000 ballots, same checks; and one GPU's
+  full share of configs[4] on 8 GPUs, 125,000 ballots, whose tally is decrypted through the
+  DecryptingTrustee shares (5 guardians, quorum 3, 2 missing: direct + compensated shares with
+  proofs checked, Lagrange combine, BSGS dLog) to the exact vote sums.
 """
 import numpy as np
 import pytest
@@ -14,7 +17,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run(group, contests, selections, nb, seed):
+def _run(group, contests, selections, nb, seed, trustees=False):
     import torch
     from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption_device, random_scalars,
                                       random_votes)
@@ -22,7 +25,7 @@ def _run(group, contests, selections, nb, seed):
     from electionguard.distributed import gather_fold_tally
     from electionguard.keyceremony import key_ceremony
     man = Manifest(contests, selections, 1)
-    gk, K = key_ceremony(group, 3, 3, seed=seed)
+    gk, K = key_ceremony(group, 5 if trustees else 3, 3, seed=seed)
     key = ElectionKey(group, K, window_bits=16)
     rng = np.random.default_rng(seed)
     votes = random_votes(rng, man, nb)
@@ -51,13 +54,19 @@ def _run(group, contests, selections, nb, seed):
 
     ok, tally = verify(0, nb)
     assert ok, "honest ballots rejected"
-    # decrypt the tally with the joint secret (quorum = all 3 guardians): t = dLog_g(beta / alpha^S)
-    S = sum(int(g.secret) for g in gk) % group.q
     T = tally.cpu().numpy()
-    M = group.powP_batch(np.ascontiguousarray(T[:, 0]), [S] * man.n_real)
-    gt = group.multP_batch(np.ascontiguousarray(T[:, 1]), group.multInv_batch(M))
-    counts = dlog_g_batch(group, gt, nb)
     want = votes.reshape(nb, man.n_contests, man.spc)[:, :, :man.n_selections].sum(axis=0).reshape(-1)
+    if trustees:  # the trustees' shares: 3 of 5 guardians available, 2 compensated
+        from electionguard.decrypt import DecryptingTrustee, Decryption
+        comm = {g.gid: g.commitments for g in gk}
+        dec = Decryption(group, qbar, [DecryptingTrustee(group, g, comm) for g in gk[:3]],
+                         [g.gid for g in gk[3:]], {g.gid: g.public_key for g in gk})
+        counts = dec.decrypt(T, nb)
+    else:  # the joint secret (quorum = all 3 guardians): t = dLog_g(beta / alpha^S)
+        S = sum(int(g.secret) for g in gk) % group.q
+        M = group.powP_batch(np.ascontiguousarray(T[:, 0]), [S] * man.n_real)
+        gt = group.multP_batch(np.ascontiguousarray(T[:, 1]), group.multInv_batch(M))
+        counts = dlog_g_batch(group, gt, nb)
     assert counts == [int(x) for x in want]
     # two-rank shard fold == the single tally
     h = nb // 2 + 17
@@ -83,3 +92,12 @@ def test_config2_one_rank_shard_125k(group):
 
 def test_config4_shape_100_selections(group):
     _run(group, 20, 5, 10_000, 23)
+
+
+@pytest.mark.timeout(600)
+def test_config4_one_rank_shard_125k_trustee_decryption(group):
+    """configs[4] (1M ballots x 100 selections over 8 GPUs): one GPU's 125,000-ballot share."""
+    import time
+    t = time.time()
+    _run(group, 20, 5, 125_000, 27, trustees=True)
+    print(f"configs[4] one-rank shard: 125,000 ballots x 120 selections, {time.time() - t:.1f} s")

@@ -55,7 +55,8 @@ def test_two_placeholders_limit_two(group, nb, monkeypatch):
     native.check(group._lib, "eg_verify_ballots", group._lib.eg_verify_ballots(
         group.handle, native.buf(int(K).to_bytes(512, "big")), native.buf(int(qbar).to_bytes(32, "big")), nb,
         man.n_contests, man.spc, 2, 1, cts.ctypes.data_as(native.c_vp), rp.ctypes.data_as(native.c_vp),
-        cp.ctypes.data_as(native.c_vp), ok_s1.ctypes.data_as(native.c_vp), ok_c1.ctypes.data_as(native.c_vp), None))
+        cp.ctypes.data_as(native.c_vp), None, ok_s1.ctypes.data_as(native.c_vp), ok_c1.ctypes.data_as(native.c_vp),
+        None))
     assert ok_s1.all() and not ok_c1.any()
     # the GPU encryptor with the oracle's injected nonces reproduces every byte
     r2 = random.Random()

@@ -22,7 +22,7 @@ def _exports():
 def test_jni_calls_every_c_abi_export():
     called = set(re.findall(r"\b(eg_[a-z0-9_]+)\s*\(", JNI_C.read_text()))
     exports = _exports()
-    assert len(exports) == 26
+    assert len(exports) == 36
     assert exports <= called, sorted(exports - called)
 
 
@@ -40,7 +40,7 @@ def test_adapters_implement_the_reference_interfaces():
                 "public List<CompensatedDecryptionAndProof> compensatedDecrypt(GroupContext group, String missingGuardianId"):
         assert sig in t, sig
     g = (JVM / "java" / "electionguard" / "gpu" / "GpuGroupContext.java").read_text()
-    for m in ("powP(", "gPowP(", "multP(", "prodP(", "multInv(", "verifyBallots(", "encryptBallots("):
+    for m in ("powP(", "gPowP(", "multP(", "prodP(", "multInv(", "verifyBallots(", "encryptBallots(", "powPAsync("):
         assert f" {m}" in g, m
 
 

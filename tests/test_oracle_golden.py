@@ -232,3 +232,73 @@ def test_c_oracle_rejects_non_residue_alpha():
     ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, man.sel_per_contest, 1, 1, cts, rp, cp, tally=False)
     assert ok_s[0].tolist() == [i != sel for i in range(len(eb.cts))]
     assert ok_c[0].tolist() == [False, True]
+
+
+# --------------------------------------------------------------------------------------
+# Spoiled ballots (RunRemoteDecryptor.java:264-269): cast-only tally and decryptBallot.
+# --------------------------------------------------------------------------------------
+
+def spoiled_case(mode=O.MODE4096):
+    d = load("spoiled.json", mode)
+    nc, ns, va = d["manifest"]
+    spc = ns + va
+    nsel = nc * spc
+    nb = len(d["ballots"])
+    cts = np.zeros((nb, nsel, 2, 512), np.uint8)
+    rp = np.zeros((nb, nsel, 4, 32), np.uint8)
+    cp = np.zeros((nb, nc, 2, 32), np.uint8)
+    for b, bal in enumerate(d["ballots"]):
+        cts[b] = _arr([x for ct in bal["cts"] for x in ct], 512).reshape(nsel, 2, 512)
+        rp[b] = _arr([x for pr in bal["rproofs"] for x in pr], 32).reshape(nsel, 4, 32)
+        cp[b] = _arr([x for pr in bal["cproofs"] for x in pr], 32).reshape(nc, 2, 32)
+    gs = [O.Guardian(f"guardian{g['x']}", g["x"], [h(a) for a in g["coeffs"]], [h(k) for k in g["commitments"]])
+          for g in d["guardians"]]
+    return d, (nc, ns, va, spc), cts, rp, cp, gs
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c_oracle_cast_only_tally_and_spoiled_plaintexts(mode):
+    """The C oracle's tally of the cast ballots alone equals the fixture's (cast-only) tally, every
+    ballot verifies, and each spoiled ballot's plaintext is its real selections' votes."""
+    from eg_oracle_c import COracle
+    G = O.production_group(mode)
+    d, (nc, ns, va, spc), cts, rp, cp, gs = spoiled_case(mode)
+    co = COracle(G.p, G.q, G.g)
+    co.set_key(h(d["K"]))
+    ok_s, ok_c, _ = co.verify_ballots(h(d["qbar"]), nc, spc, va, va, cts, rp, cp, threads=2, tally=False)
+    assert ok_s.all() and ok_c.all()
+    cast = np.array(d["cast"], bool)
+    _, _, tally = co.verify_ballots(h(d["qbar"]), nc, spc, va, va, cts[cast], rp[cast], cp[cast], threads=2)
+    assert [[t[0].tobytes().hex(), t[1].tobytes().hex()] for t in tally] == d["tally"]
+    for bal, c in zip(d["ballots"], d["cast"]):
+        if not c:
+            assert bal["plaintext"] == [bal["votes"][k * spc + s] for k in range(nc) for s in range(ns)]
+    assert K_of(gs, G) == h(d["K"])
+
+
+def K_of(gs, G):
+    return G.prodP([g.K for g in gs])
+
+
+def test_python_oracle_reproduces_spoiled_decryption():
+    """decryptBallot restated (oracle.decrypt_ballot) reproduces every share, proof, recovery key
+    and plaintext of the fixture from the guardians' coefficients and the injected nonces."""
+    G = O.production_group()
+    d, (nc, ns, va, spc), cts, rp, cp, gs = spoiled_case()
+    man = O.Manifest(nc, ns, va)
+    qbar = h(d["qbar"])
+    avail = [g for g in gs if g.gid in d["available"]]
+    missing = [g for g in gs if g.gid in d["missing"]]
+    for b, (bal, c) in enumerate(zip(d["ballots"], d["cast"])):
+        if c:
+            continue
+        eb = O.EncryptedBallot([O.Ciphertext(h(a), h(x)) for a, x in bal["cts"]], [], [])
+        plain, shares = O.decrypt_ballot(G, qbar, man, eb, avail, missing, [h(u) for u in bal["nonces"]])
+        assert plain == bal["plaintext"]
+        for gid, lst in shares["direct"].items():
+            assert [(hex(M), hex(p.c), hex(p.v)) for M, p in lst] == \
+                [(hex(h(w["M"])), hex(h(w["c"])), hex(h(w["v"]))) for w in bal["direct"][gid]]
+        for l, by in shares["compensated"].items():
+            for gid, lst in by.items():
+                assert [(M, p.c, p.v, rk) for M, p, rk in lst] == \
+                    [(h(w["M"]), h(w["c"]), h(w["v"]), h(w["recovery"])) for w in bal["compensated"][l][gid]]

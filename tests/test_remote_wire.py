@@ -132,3 +132,30 @@ def test_ten_thousand_texts_fit_default_channel_limits():
         px.close()
     finally:
         srv.stop()
+
+
+class ShortTrustee(EchoTrustee):
+    """Echo stand-in that drops the last result of its second batch without reporting an error."""
+
+    def directDecrypt(self, group, texts, qbar, nonce=None):
+        res = super().directDecrypt(group, texts, qbar, nonce)
+        return res[:-1] if len(self.calls) == 2 else res
+
+
+def test_short_batch_without_error_fails_the_whole_call():
+    """A trustee answering one of the proxy's RPCs with fewer results than texts (and no error
+    string) must not shift the later results onto the wrong texts: the proxy returns the
+    reference's failure value, an empty list (RemoteDecryptingTrusteeProxy.java:64-66)."""
+    from electionguard.remote import DecryptingTrusteeServer, RemoteDecryptingTrusteeProxy
+    G = O.production_group()
+    rng = random.Random(5)
+    texts = [(rng.randrange(G.p), rng.randrange(G.p)) for _ in range(9)]
+    tr = ShortTrustee(G.q)
+    srv = DecryptingTrusteeServer(None, tr).start()
+    try:
+        px = RemoteDecryptingTrusteeProxy("g1", f"127.0.0.1:{srv.port}", 1, 1, max_texts_per_rpc=4)
+        assert px.directDecrypt(None, texts, 7) == []
+        assert tr.calls == [4, 4]  # the third RPC is never sent
+        px.close()
+    finally:
+        srv.stop()

@@ -7,6 +7,9 @@
   4 remote decryption: one trustee PROCESS per available guardian over gRPC on localhost,
     missing guardians compensated (RunRemoteDecryptionTest.java:63-136)
   5 check the decrypted counts against the plaintext votes (the reference only prints)
+  6 with -nspoiled k: the first k ballots are spoiled -- verified but not tallied, then each is
+    decrypted through the same remote trustees (RunRemoteDecryptor.java:264-269, -decryptSpoiled)
+    and must decrypt to its own votes
 
     python tools/run_workflow.py -nguardians 3 -quorum 3 -nballots 25            # configs[0]
     python tools/run_workflow.py -nguardians 5 -quorum 3 -navailable 3 -nballots 100   # configs[3]
@@ -40,7 +43,10 @@ def main():
     ap.add_argument("-fbwindow", type=int, default=8, help="fixed-base radix window bits for K (8 = LOW_MEMORY_USE)")
     ap.add_argument("-chunk", type=int, default=65536,
                     help="ballots per encrypt+verify batch; batch tallies are multiplied (bounded memory)")
+    ap.add_argument("-nspoiled", type=int, default=0, help="spoiled ballots (the first k; at most one chunk)")
     a = ap.parse_args()
+    if a.nspoiled > min(a.chunk, a.nballots):
+        ap.error("-nspoiled must fit in the first chunk")
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
     from electionguard.core import productionGroup
     from electionguard.decrypt import Decryption, verify_decryption_record
@@ -66,19 +72,28 @@ def main():
     ver = Verifier(G, key, qbar, man)
     expected = np.zeros(man.n_real, dtype=np.int64)
     tally, t_enc, t_ver, t_gen, all_ok = None, 0.0, 0.0, 0.0, True
+    spoiled, spoiled_votes = None, None
     for b0 in range(0, a.nballots, a.chunk):
         nb = min(a.chunk, a.nballots - b0)
         t = time.time()
         votes = random_votes(rng, man, nb)
         sn = random_scalars(rng, (nb, man.nsel, 4), G.q)
         cn = random_scalars(rng, (nb, man.n_contests), G.q)
-        expected += votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].sum(axis=0, dtype=np.int64).reshape(-1)
+        cast = np.ones(nb, bool)
+        if b0 == 0:
+            cast[: a.nspoiled] = False
+        real = votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].reshape(nb, man.n_real)
+        expected += real[cast].sum(axis=0, dtype=np.int64)
+        if b0 == 0 and a.nspoiled:
+            spoiled_votes = real[~cast]
         t_gen += time.time() - t
         t = time.time()
         eb = batch_encryption(G, key, qbar, man, votes, sn, cn)
         t_enc += time.time() - t
+        if b0 == 0 and a.nspoiled:
+            spoiled = eb.slice(0, a.nspoiled)
         t = time.time()
-        ok_s, ok_c, part = ver.verify(eb)
+        ok_s, ok_c, part = ver.verify(eb, cast=None if cast.all() else cast)
         all_ok = all_ok and bool(ok_s.all() and ok_c.all())
         tally = part if tally is None else G.multP_batch(tally.reshape(-1, 512), part.reshape(-1, 512)).reshape(part.shape)
         t_ver += time.time() - t
@@ -112,9 +127,21 @@ def main():
         rv = verify_decryption_record(G, qbar, rec, {g.gid: g.public_key for g in gk}, comm)
         print(f"*** verify decryption record {time.time() - t:.3f} s: {rv}")
         ok = counts == [int(x) for x in expected]
-        print(json.dumps({"counts": counts, "expected": [int(x) for x in expected], "match": ok,
-                          "record_checks": rv,
+        spoiled_ok, rvs = True, {}
+        if spoiled is not None:
+            t = time.time()
+            srec = dec.decrypt_ballots_record(spoiled, man)
+            plain = np.array([-1 if c is None else c for c in srec.counts]).reshape(-1, man.n_real)
+            spoiled_ok = bool(np.array_equal(plain, spoiled_votes))
+            rvs = verify_decryption_record(G, qbar, srec, {g.gid: g.public_key for g in gk}, comm,
+                                           max_count=man.votes_allowed)
+            print(f"*** decryptBallot x {a.nspoiled} spoiled ({a.nspoiled * man.n_real} selections, one remote batch "
+                  f"per trustee) {time.time() - t:.3f} s: plaintexts match = {spoiled_ok}, record = {rvs}")
+        print(json.dumps({"counts": counts, "expected": [int(x) for x in expected], "match": ok and spoiled_ok,
+                          "record_checks": rv, "spoiled": a.nspoiled, "spoiled_match": spoiled_ok,
+                          "spoiled_record_checks": rvs,
                           "all_took_s": round(time.time() - t_all, 3)}))
+        ok = ok and spoiled_ok and all(rvs.values())
         for px in proxies:
             px.finish(ok)
         for p in procs:
