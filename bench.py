@@ -139,7 +139,7 @@ def main():
     torch.cuda.synchronize()
     enc_dev = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev)
     enc_dev_ct = None
-    if a.ct_encrypt:  # constant-time mode (masked table scans, no secret-indexed address): same bytes
+    if a.ct_encrypt and world == 1:  # constant-time mode (masked table scans, no secret-indexed address): same bytes
         group.ct_encrypt = True
         try:
             enc_dev_ct = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2)

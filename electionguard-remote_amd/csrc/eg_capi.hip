@@ -141,6 +141,12 @@ struct eg_fixed_base {
   FbTab tab() const { return FbTab{d_tab, (uint32_t)wbits, (uint32_t)nwin}; }
 };
 
+// widest radix table a constant-time fixed-base term scans (2^w entries per multiply)
+constexpr uint32_t kCtMaxWindow = 8;
+// radix width of the constant-time encryption tables of g and K (eg_ctx_set_ct_encrypt): 43
+// windows of 64 entries, 1.76 MB per base (EG_CT_WINDOW=4..8 overrides it at context creation)
+constexpr int kCtEncWindow = 6;
+
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
   W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_RC, W_CRF, W_CAST, W_NSLOT
@@ -170,6 +176,7 @@ struct eg_ctx {
   std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
   uint32_t ct_encrypt = 0;              // encryption on k_pow<F, true> with small CT tables (eg_ctx_set_ct_encrypt)
+  int ct_window = kCtEncWindow;         // their radix width
   eg_fixed_base *g_ct = nullptr, *K_ct = nullptr;  // their kCtEncWindow-bit tables of g and K
   uint8_t K_ct_be[512];
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
@@ -401,11 +408,6 @@ static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const
 // sub-launch so its short jobs fill that launch's tail (PowPart in eg_kernels.hpp).
 // jobs per k_pow sub-launch (bounds the per-launch scratch: 32 or 64 comb entries per job)
 constexpr size_t kPowMaxJobs = (size_t)1 << 18;
-// widest radix table a constant-time fixed-base term scans (2^w entries per multiply)
-constexpr uint32_t kCtMaxWindow = 8;
-// radix width of the constant-time encryption tables of g and K (eg_ctx_set_ct_encrypt):
-// 43 windows of 64 entries, 1.76 MB per base
-constexpr int kCtEncWindow = 6;
 
 struct PowTail {
   PowShape S;
@@ -668,6 +670,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   }
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
   if (const char* cr = getenv("EG_CT_ROWS")) c->ct_rows = (cr[0] == '5') ? 0u : 4u;
+  if (const char* cw = getenv("EG_CT_WINDOW")) c->ct_window = std::max(4, std::min((int)kCtMaxWindow, atoi(cw)));
   {
     int cus = 0, per_cu = 0;
     const char* ts = getenv("EG_TAIL_SPLIT");
