@@ -7,10 +7,14 @@ path produces.  Every exponentiation runs on the GPU through the C ABI:
                          (keyceremony.verify_commitment_proofs);
   * ``joint_key``        K == prod_i K_i0;
   * ``ballots``          every disjunctive and contest proof of every ballot (eg_verify_ballots);
-  * ``tally``            the published encrypted tally == the product of the ballots'
+  * ``tally``            the published encrypted tally == the product of the CAST ballots'
                          ciphertexts per real selection (runAccumulateBallots, :151);
   * ``decryption.*``     decrypt.verify_decryption_record (share proofs, recovery keys,
-                         quorum, B == M g^t).
+                         quorum, B == M g^t, counts <= the number of cast ballots);
+  * ``spoiled.*``        with spoiled ballots (``cast`` flags): their decryption record covers
+                         exactly their real selections (``spoiled.texts``) and passes the same
+                         share / quorum / B == M g^t checks with values <= votesAllowed
+                         (decryptBallot, RunRemoteDecryptor.java:264-269).
 
 Manifest, hash-chain and protobuf-format checks are record plumbing outside the hot path
  and are not restated.
@@ -18,13 +22,13 @@ Manifest, hash-chain and protobuf-format checks are record plumbing outside the 
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
 from .ballot import ElectionKey, EncryptedBallots, Manifest, Verifier
 from .core.group import GroupContext, as_p_array
-from .decrypt import DecryptionRecord, verify_decryption_record
+from .decrypt import DecryptionRecord, spoiled_texts, verify_decryption_record
 from .keyceremony import verify_commitment_proofs
 
 
@@ -43,8 +47,10 @@ class ElectionRecord:
     joint_key: int                  # K
     guardians: List[GuardianRecord]
     ballots: EncryptedBallots
-    encrypted_tally: np.ndarray     # (n_real, 2, 512)
+    encrypted_tally: np.ndarray     # (n_real, 2, 512), over the cast ballots
     decryption: DecryptionRecord
+    cast: Optional[np.ndarray] = None                   # (nb,) bool; None = every ballot cast
+    spoiled_decryption: Optional[DecryptionRecord] = None  # the spoiled ballots' selections
 
 
 def verify_election_record(group: GroupContext, rec: ElectionRecord, window_bits: int = 8) -> Dict[str, bool]:
@@ -65,8 +71,13 @@ def verify_election_record(group: GroupContext, rec: ElectionRecord, window_bits
         out["joint_key"] = False
     man = rec.manifest
     key = ElectionKey(group, rec.joint_key, window_bits=window_bits)
-    ok_s, ok_c, tally = Verifier(group, key, rec.qbar, man).verify(rec.ballots)
-    out["ballots"] = bool(ok_s.all() and ok_c.all())
+    nb = rec.ballots.n
+    cast = np.ones(nb, bool) if rec.cast is None else np.asarray(rec.cast, bool).reshape(-1)
+    cast_ok = cast.shape == (nb,)
+    if not cast_ok:
+        cast = np.ones(nb, bool)
+    ok_s, ok_c, tally = Verifier(group, key, rec.qbar, man).verify(rec.ballots, cast=cast)
+    out["ballots"] = bool(ok_s.all() and ok_c.all()) and cast_ok
     et = np.ascontiguousarray(rec.encrypted_tally, dtype=np.uint8).reshape(-1, 2, 512)
     out["tally"] = et.shape == tally.shape and bool(np.array_equal(et, tally))
     dtexts = np.ascontiguousarray(rec.decryption.texts, dtype=np.uint8).reshape(-1, 2, 512)
@@ -76,8 +87,22 @@ def verify_election_record(group: GroupContext, rec: ElectionRecord, window_bits
     dv = verify_decryption_record(group, rec.qbar, rec.decryption, pks, commitments,
                                   guardian_xs={g.gid: g.x for g in rec.guardians},
                                   quorum=len(rec.guardians[0].commitments) if shapes_ok else None,
-                                  max_count=rec.ballots.n)
+                                  max_count=int(cast.sum()))
     out["decryption.texts"] = same_texts
     for name, ok in dv.items():
         out[f"decryption.{name}"] = ok
+    if (~cast).any() or rec.spoiled_decryption is not None:
+        sp = rec.spoiled_decryption
+        want = spoiled_texts(man, rec.ballots.cts[~cast])
+        got = None if sp is None else np.ascontiguousarray(sp.texts, dtype=np.uint8).reshape(-1, 2, 512)
+        out["spoiled.texts"] = got is not None and got.shape == want.shape and bool(np.array_equal(got, want))
+        if sp is None or not len(want):
+            out["spoiled.decryption"] = sp is None and not len(want)
+        else:
+            sv = verify_decryption_record(group, rec.qbar, sp, pks, commitments,
+                                          guardian_xs={g.gid: g.x for g in rec.guardians},
+                                          quorum=len(rec.guardians[0].commitments) if shapes_ok else None,
+                                          max_count=man.votes_allowed)
+            for name, ok in sv.items():
+                out[f"spoiled.{name}"] = ok
     return out

@@ -113,3 +113,48 @@ def test_structurally_bad_records_report_false_instead_of_raising(group, electio
     gone = sorted(bad.decryption.direct)[0]
     del bad.decryption.direct[gone]   # 2 available < quorum 3, and gone is neither available nor missing
     assert "decryption.quorum" in _failed(verify_election_record(group, bad))
+
+
+def test_record_with_spoiled_ballots(group):
+    """A record with 3 spoiled ballots of 12 (RunRemoteDecryptor.java:264-269): the tally covers the
+    9 cast ones, the spoiled ballots' decryption covers exactly their real selections and passes
+    every share check with plaintexts <= votesAllowed; claiming a spoiled ballot as cast breaks
+    the tally, and a tampered spoiled plaintext breaks only the spoiled record's B == M g^t."""
+    from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
+    from electionguard.decrypt import DecryptingTrustee, Decryption
+    from electionguard.keyceremony import key_ceremony
+    from electionguard.record import ElectionRecord, GuardianRecord, verify_election_record
+    gk, K = key_ceremony(group, 5, 3, seed=78)
+    man = Manifest(2, 3, 1)
+    rng = np.random.default_rng(78)
+    nb = 12
+    votes = random_votes(rng, man, nb)
+    qbar = 0xABCDE0
+    key = ElectionKey(group, K)
+    eb = batch_encryption(group, key, qbar, man, votes, random_scalars(rng, (nb, man.nsel, 4), group.q),
+                          random_scalars(rng, (nb, man.n_contests), group.q))
+    cast = np.ones(nb, bool)
+    cast[[1, 6, 11]] = False
+    _, _, tally = Verifier(group, key, qbar, man).verify(eb, cast=cast)
+    comm = {g.gid: g.commitments for g in gk}
+    dec = Decryption(group, qbar, [DecryptingTrustee(group, g, comm) for g in gk[:3]], [g.gid for g in gk[3:]],
+                     {g.gid: g.public_key for g in gk})
+    drec = dec.decrypt_record(tally, int(cast.sum()))
+    srec = dec.decrypt_ballots_record(eb.slice(0, nb).cts[~cast], man)
+    real = votes.reshape(nb, man.n_contests, man.spc)[:, :, : man.n_selections].reshape(nb, man.n_real)
+    assert drec.counts == [int(x) for x in real[cast].sum(axis=0)]
+    assert np.array_equal(np.array(srec.counts).reshape(-1, man.n_real), real[~cast])
+    rec = ElectionRecord(man, qbar, K, [GuardianRecord(g.gid, g.x, list(g.commitments), list(g.proofs)) for g in gk],
+                         eb, tally, drec, cast=cast, spoiled_decryption=srec)
+    res = verify_election_record(group, rec)
+    assert all(res.values()) and "spoiled.tally" in res, res
+    bad = copy.copy(rec)
+    bad.cast = np.ones(nb, bool)  # the spoiled ballots claimed as cast
+    assert "tally" in _failed(verify_election_record(group, bad))
+    bad = copy.copy(rec)
+    bad.spoiled_decryption = copy.deepcopy(srec)
+    bad.spoiled_decryption.counts[4] = 1 - bad.spoiled_decryption.counts[4]
+    assert _failed(verify_election_record(group, bad)) == ["spoiled.tally"]
+    bad = copy.copy(rec)
+    bad.spoiled_decryption = None
+    assert _failed(verify_election_record(group, bad)) == ["spoiled.decryption", "spoiled.texts"]
