@@ -271,3 +271,34 @@ def test_launch_split_independent(group, slots, monkeypatch):
     ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, cp), with_tally=False)
     assert np.argwhere(~ok_s).tolist() == [[3, 7]]
     assert np.argwhere(~ok_c).tolist() == [[650, 1]]
+
+
+def test_cast_mask_across_verify_chunks(group):
+    """The cast flags follow each ballot across the verifier's 16,384-ballot chunks, on the
+    host-pointer path (flags uploaded once, offset per chunk) and the device path: spoiled
+    ballots on both sides of the boundary, the tally equals the CPython product over the cast
+    ballots only; the verdicts of every ballot are still computed."""
+    import torch
+    from electionguard.ballot import EncryptedBallots, Manifest, Verifier
+    man = Manifest(1, 2, 1)
+    nb = 16384 + 300
+    key, K, qbar, eb = _encrypt(group, man, nb, 53)
+    rng = np.random.default_rng(53)
+    cast = rng.random(nb) > 0.25
+    cast[[16383, 16384]] = (False, False)
+    V = Verifier(group, key, qbar, man)
+    ok_s, ok_c, tally = V.verify(eb, cast=cast)
+    assert ok_s.all() and ok_c.all()
+    want = _tally_products(man, EncryptedBallots(eb.cts[cast], eb.rproof[cast], eb.cproof[cast]))
+    assert np.array_equal(tally, want)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (eb.cts, eb.rproof, eb.cproof)]
+    dm = torch.from_numpy(cast.astype(np.uint8)).to(dev)
+    oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
+    okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
+    tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    V.verify_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), nb, oks.data_ptr(), okc.data_ptr(),
+                    tal.data_ptr(), dm.data_ptr())
+    group.sync()
+    assert bool(oks.all()) and bool(okc.all()) and np.array_equal(tal.cpu().numpy(), want)
