@@ -37,7 +37,7 @@ namespace eg {
 #endif
 constexpr int kLimbBits = EG_RADIX;
 constexpr uint32_t kMask = (1u << kLimbBits) - 1u;
-constexpr int kN = EG_RADIX == 29 ? 144 : 152;  // limbs per element (R = 2^(kN*kLimbBits) > 4p)
+constexpr int kN = EG_RADIX == 29 ? 144 : (EG_RADIX == 28 ? 148 : 152);  // limbs per element (R = 2^(kN*kLimbBits) > 4p)
 constexpr int kT = EG_T;              // lanes per element
 constexpr int kL = kN / kT;           // limbs per lane
 constexpr int kLP = (kL + 3) & ~3;    // padded limbs per lane (16-B aligned lane blocks)
@@ -46,11 +46,11 @@ constexpr int kYStride = kW + 4;      // LDS words per group slot (bank spread)
 constexpr int kWave = 64;
 constexpr int kGroupsPerWave = kWave / kT;
 static_assert(kN % kT == 0, "limbs must split evenly over the group");
-static_assert(EG_RADIX == 27 || EG_RADIX == 29, "radix 2^27 (152 limbs) or 2^29 (144 limbs)");
+static_assert(EG_RADIX >= 27 && EG_RADIX <= 29, "radix 2^27 (152 limbs), 2^28 (148) or 2^29 (144 limbs)");
 static_assert(kN * kLimbBits >= 4098, "R must exceed 4p (lazy reduction: values stay < 2p)");
 // Accumulator headroom: a register lives L steps in its lane and takes <= 2 products per step
 // (x*y + m*p; with SQR one doubled x*x product + m*p).  Radix 2^29 needs L <= 18.
-static_assert(EG_RADIX == 27 || kL <= 18, "radix 2^29 overflows the 64-bit columns above 18 limbs per lane");
+static_assert((unsigned __int128)2 * kL * (((1ull << kLimbBits) + 64) * ((1ull << kLimbBits) + 64)) < ((unsigned __int128)1 << 64), "radix 2^29 overflows the 64-bit columns above 18 limbs per lane");
 static_assert(kT == 4 || kT == 8, "EG_T must be 4 or 8");
 static_assert(kW == 160, "device element format is 160 words");
 
@@ -171,68 +171,83 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t v) {
 // with per-lane (offset, width).  L = 18: 9.5 MACs + 1 VALU instead of 18.  All contributions
 // to column c still arrive by step c (each pair is added at row <= c), so the CIOS
 // quotient digits are unchanged.
+// One CIOS step at register rotation r (multiplier digit yi): t += x * yi, then t += m * p and
+// the lowest column's split.  FIRST: the multiply's very first step, whose accumulator is
+// implicitly zero -- the products are written instead of added (no zeroing pass; for SQR the
+// registers the half-row leaves untouched are first written by the m * p half).
+template <bool FRIENDLY, bool SQR, bool FIRST, class PT>
+__device__ __forceinline__ void cios_step(uint64_t (&acc)[kL], const uint32_t (&x)[kL], const int r, const uint32_t yi,
+                                          const PT& p, uint32_t n0, uint32_t mask, uint32_t doff, uint32_t dwid) {
+  // t += x * y_i     (logical position j lives in register (j + r) % L)
+  int jmax = 0;
+  if constexpr (SQR) {
+    {
+      const uint32_t d = __builtin_amdgcn_ubfe(x[r], doff, dwid);
+      uint64_t& A = acc[(r + r) % kL];
+      A = FIRST ? (uint64_t)d * yi : (uint64_t)d * yi + A;
+    }
+    // odd L: offsets 1..(L-1)/2; even L: offsets 1..L/2-1, plus the offset-L/2 pair
+    // at the row with the smaller register index (r < L/2)
+    constexpr int kHalf = (kL - 1) / 2;
+    jmax = (kL % 2 == 1) ? kHalf : (r < kL / 2 ? kL / 2 : kL / 2 - 1);
+#pragma unroll
+    for (int jj = 1; jj <= jmax; ++jj) {
+      const int j = (r + jj) % kL;
+      uint64_t& A = acc[(j + r) % kL];
+      A = FIRST ? (uint64_t)x[j] * yi : (uint64_t)x[j] * yi + A;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kL; ++j) {
+      uint64_t& A = acc[(j + r) % kL];
+      A = FIRST ? (uint64_t)x[j] * yi : (uint64_t)x[j] * yi + A;
+    }
+  }
+  // quotient digit from the group's lowest limb
+  uint32_t t0 = (uint32_t)acc[r % kL];
+  if constexpr (!FRIENDLY) t0 *= n0;
+  const uint32_t m = bcast_g0_and(t0, mask);
+  // t += m * p   (FIRST, SQR: registers (r + 1 + jmax .. r + L - 1) % L are still unwritten;
+  // with r = 0 those are the ones whose register index exceeds jmax)
+#pragma unroll
+  for (int j = 0; j < kL; ++j) {
+    uint64_t& A = acc[(j + r) % kL];
+    const bool fresh = FIRST && SQR && ((j + r) % kL) > r + jmax;
+    A = fresh ? (uint64_t)p[j] * m : (uint64_t)p[j] * m + A;
+  }
+  // split the lowest column: carry stays in this lane (next position),
+  // low 27 bits shift into lane-1's top position (0 for the group's lane 0)
+  uint64_t& A0 = acc[r % kL];
+  acc[(r + 1) % kL] += A0 >> kLimbBits;
+  A0 = (uint64_t)from_next_and((uint32_t)A0, mask);
+}
+
 template <bool FRIENDLY, bool SQR, class PT>
 __device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t* __restrict__ y,
                                               const PT& p, uint32_t n0, uint32_t mask) {
   uint64_t acc[kL];
-#pragma unroll
-  for (int j = 0; j < kL; ++j) acc[j] = 0;
   if constexpr (SQR) {
 #pragma unroll
     for (int j = 0; j < kL; ++j) x[j] <<= 1;  // 2x < 2^(b+1) + 2^(65-2b) < 2^31
   }
-
+  // SQR: the diagonal multiplier of outer block s is x_r (own row: (2x_r) >> 1) on lane s,
+  // 2x_r on the lanes above and 0 below (width 0); carried from trip to trip
+  const int gl = glane();
+  uint32_t doff = SQR && gl == 0 ? 1u : 0u, dwid = SQR ? 31u : 0u;
+  // the first step runs peeled (no accumulator zeroing); every trip s then runs its steps
+  // 1..L-1 and the next trip's step 0 (same register rotation: r = 0 follows r = L-1)
+  cios_step<FRIENDLY, SQR, true>(acc, x, 0, y[0], p, n0, mask, doff, dwid);
 #pragma unroll 1
   for (int s = 0; s < kT; ++s) {
     const uint32_t* ys = y + s * kLP;
-    uint32_t doff = 0, dwid = 0;
-    if constexpr (SQR) {
-      const int gl = glane();
-      doff = (gl == s) ? 1u : 0u;   // own row: x_r = (2x_r) >> 1
-      dwid = (gl >= s) ? 31u : 0u;  // rows above: 2x_r (< 2^31); rows below: 0 (width 0)
-    }
 #pragma unroll
-    for (int r = 0; r < kL; ++r) {
-      const uint32_t yi = ys[r];
-      // t += x * y_i     (logical position j lives in register (j + r) % L)
+    for (int r = 1; r < kL; ++r) cios_step<FRIENDLY, SQR, false>(acc, x, r, ys[r], p, n0, mask, doff, dwid);
+    if (s + 1 < kT) {
       if constexpr (SQR) {
-        {
-          const uint32_t d = __builtin_amdgcn_ubfe(x[r], doff, dwid);
-          uint64_t& A = acc[(r + r) % kL];
-          A = (uint64_t)d * yi + A;
-        }
-        // odd L: offsets 1..(L-1)/2; even L: offsets 1..L/2-1, plus the offset-L/2 pair
-        // at the row with the smaller register index (r < L/2)
-        constexpr int kHalf = (kL - 1) / 2;
-        const int jmax = (kL % 2 == 1) ? kHalf : (r < kL / 2 ? kL / 2 : kL / 2 - 1);
-#pragma unroll
-        for (int jj = 1; jj <= jmax; ++jj) {
-          const int j = (r + jj) % kL;
-          uint64_t& A = acc[(j + r) % kL];
-          A = (uint64_t)x[j] * yi + A;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < kL; ++j) {
-          uint64_t& A = acc[(j + r) % kL];
-          A = (uint64_t)x[j] * yi + A;
-        }
+        doff = (gl == s + 1) ? 1u : 0u;
+        dwid = (gl >= s + 1) ? 31u : 0u;
       }
-      // quotient digit from the group's lowest limb
-      uint32_t t0 = (uint32_t)acc[r % kL];
-      if constexpr (!FRIENDLY) t0 *= n0;
-      const uint32_t m = bcast_g0_and(t0, mask);
-      // t += m * p
-#pragma unroll
-      for (int j = 0; j < kL; ++j) {
-        uint64_t& A = acc[(j + r) % kL];
-        A = (uint64_t)p[j] * m + A;
-      }
-      // split the lowest column: carry stays in this lane (next position),
-      // low 27 bits shift into lane-1's top position (0 for the group's lane 0)
-      uint64_t& A0 = acc[r % kL];
-      acc[(r + 1) % kL] += A0 >> kLimbBits;
-      A0 = (uint64_t)from_next_and((uint32_t)A0, mask);
+      cios_step<FRIENDLY, SQR, false>(acc, x, 0, ys[kLP], p, n0, mask, doff, dwid);
     }
   }
   // two parallel carry passes -> limbs < 2^27 + 2^11 (enough headroom for the next op)

@@ -18,6 +18,9 @@ constexpr int kBlock = 256;
 #ifndef EG_MASK_RT
 #define EG_MASK_RT 2  // 2: limb mask pinned in a VGPR so both per-step ANDs fold into v_and_b32_dpp
 #endif
+#ifndef EG_TRAFFIC_X2
+#define EG_TRAFFIC_X2 0  // A/B probe: extra HBM traffic at equal VALU count (never in production builds)
+#endif
 #ifndef EG_MIN_WAVES
 #define EG_MIN_WAVES 3  // k_pow: 3 waves/SIMD (<= 168 VGPRs; a few squaring-loop spills, measured +1.3..1.6%)
 #endif
@@ -638,6 +641,22 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         else elem_to_lds(slot, ysrc);
       } else {
         elem_to_lds(slot, ysrc);
+#if EG_TRAFFIC_X2
+        // A/B probe only (tools/ab_mm.py): every comb multiply also reads the same entry of the
+        // table of a job 7 workgroups away (an L2 miss) into a discarded LDS block, adding ~60%
+        // HBM traffic at nearly equal VALU count
+        if (kind == OP_MUL_COMB && !S.shared_comb) {
+          __shared__ uint32_t s_sink[kGroupsPerBlock * kT];
+          const uint32_t ngr = P.nblocks * kGroupsPerBlock;
+          const uint32_t og = (gid + 7u * kGroupsPerBlock) % ngr;
+          const uint32_t* far = P.scratch + (size_t)og * tsize * kW + (size_t)dig[arg] * kW;
+          const uint32_t* src = far + glane() * kLP;
+          uint32_t acc = 0;
+#pragma unroll 1
+          for (int j = 0; j < kLP; j += 4) acc ^= src[j] ^ src[j + 1] ^ src[j + 2] ^ src[j + 3];
+          reinterpret_cast<volatile uint32_t*>(s_sink)[threadIdx.x] = acc;
+        }
+#endif
       }
       wave_sync();
       M.mul(x, slot);
