@@ -188,8 +188,9 @@ struct eg_ctx {
   // most recently used first
   std::vector<std::pair<std::array<uint8_t, 512>, eg_fixed_base*>> share_keys;
   // per-element calls from many threads gathered into batches (eg_capi_coalesce.inc)
-  struct Coalescer* co = nullptr;
+  std::shared_ptr<struct Coalescer> co;  // tickets share it: waiting stays valid after the ctx is gone
   std::mutex co_mu;  // guards the lazy creation of co
+  bool co_closed = false;  // set by eg_ctx_destroy (under co_mu)
   // host-pointer verify: uploads of chunk k+1 on their own stream overlap chunk k's kernels
   hipStream_t copy = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};

@@ -81,3 +81,24 @@ def test_coalescing_window_and_errors(group):
     group.set_coalescing(16384, 100)
     with pytest.raises(native.EgError):
         group.set_coalescing(0, 100)
+
+
+def test_ticket_outlives_context(group):
+    """A ticket submitted before eg_ctx_destroy stays waitable after it: destroy drains the open
+    batches, and the ticket keeps the dispatcher's state alive."""
+    import ctypes
+    from electionguard.core import native
+    lib = native.load()
+    h = ctypes.c_void_p()
+    native.check(lib, "eg_ctx_create", lib.eg_ctx_create(native.buf(group._p_be), native.buf(group._q_be),
+                                                         native.buf(group._g_be), group.device, ctypes.byref(h)))
+    native.check(lib, "eg_ctx_set_coalescing", lib.eg_ctx_set_coalescing(h, 16384, 200000))  # 0.2 s window
+    base, e = 0x1234567, 0xABCDEF
+    out = bytearray(512)
+    t = ctypes.c_void_p()
+    native.check(lib, "eg_powp_submit", lib.eg_powp_submit(h, native.buf(base.to_bytes(512, "big")),
+                                                           native.buf(e.to_bytes(32, "big")), native.buf(out),
+                                                           ctypes.byref(t)))
+    native.check(lib, "eg_ctx_destroy", lib.eg_ctx_destroy(h))  # drains the batch before returning
+    native.check(lib, "eg_ticket_wait", lib.eg_ticket_wait(t))
+    assert int.from_bytes(out, "big") == pow(base, e, group.p)
