@@ -149,7 +149,7 @@ constexpr int kCtEncWindow = 6;
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_RC, W_CRF, W_CAST, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_CRF, W_CAST, W_NSLOT
 };
 
 struct eg_ctx {

@@ -340,6 +340,20 @@ __global__ void __launch_bounds__(kBlock) k_resid_check(const MontConsts* __rest
   }
 }
 
+// A contest's message flags (A, B) = (prod alpha_i, prod beta_i) from its selections' flags: the
+// order-q subgroup is closed under products, so A is a valid residue when every alpha_i is one
+// (range + residue flags, k_import / k_resid_check), and a contest with an invalid selection is
+// rejected with it.  One thread per (contest, component); flags[(j spc + s) * 2 + comp].
+__global__ void __launch_bounds__(kBlock) k_contest_flags(const uint8_t* __restrict__ sel_flags, uint32_t ncn,
+                                                          uint32_t spc, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncn * 2) return;
+  const size_t base = (size_t)(i >> 1) * spc * 2 + (i & 1u);
+  uint8_t ok = 1;
+  for (uint32_t s = 0; s < spc; ++s) ok &= sel_flags[base + (size_t)s * 2];
+  out[i] = ok;
+}
+
 // out[i*so] = a[i*sa] * b[i*sb]  (Montgomery form; strides in elements)
 template <bool F>
 __global__ void __launch_bounds__(kBlock) k_mul(const MontConsts* __restrict__ C,

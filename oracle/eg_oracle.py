@@ -291,10 +291,9 @@ def make_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, R_sum: int,
 
 
 def verify_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, limit: int, pr: GenericProof) -> bool:
-    """Contest selection-limit proof over the aggregate message (A, B) = (prod alpha, prod beta);
-    like the range proof it requires the message to be valid residues."""
-    if not (is_valid_residue(G, A) and is_valid_residue(G, B)):
-        return False
+    """Contest selection-limit proof over the aggregate message (A, B) = (prod alpha, prod beta).
+    The message's validity is checked by the caller on its factors (verify_ballot): the order-q
+    subgroup is closed under products, so (A, B) are valid residues when every selection is."""
     if not (0 <= pr.c < G.q and 0 <= pr.v < G.q):
         return False
     a, b = constant_commitments(G, K, A, B, limit, pr)
@@ -365,9 +364,11 @@ def verify_ballot(G: Group, K: int, qbar: int, man: Manifest, eb: EncryptedBallo
         for s in range(spc):
             i = c * spc + s
             ok &= verify_range_proof(G, K, qbar, eb.cts[i], eb.proofs[i])
-        A = G.prodP([ct.pad for ct in eb.cts[c * spc:(c + 1) * spc]])
-        B = G.prodP([ct.data for ct in eb.cts[c * spc:(c + 1) * spc]])
-        ok &= verify_constant_proof(G, K, qbar, A, B, man.votes_allowed, eb.contest_proofs[c])
+        sel = eb.cts[c * spc:(c + 1) * spc]
+        A = G.prodP([ct.pad for ct in sel])
+        B = G.prodP([ct.data for ct in sel])
+        msg_ok = all(is_valid_residue(G, ct.pad) and is_valid_residue(G, ct.data) for ct in sel)
+        ok &= msg_ok and verify_constant_proof(G, K, qbar, A, B, man.votes_allowed, eb.contest_proofs[c])
     return ok
 
 

@@ -75,7 +75,8 @@ def _ballot_arrays(eb):
 
 def test_gpu_rejects_non_residue_alpha_with_matching_proofs(group):
     """alpha * (p-1) with every Fiat-Shamir equation re-made to hold (c even): only the
-    x^q == 1 tests catch it, for the selection (alpha) and for its contest (A = prod alpha).
+    x^q == 1 tests catch it, for the selection (alpha) and for its contest (A = prod alpha, valid
+    only when every alpha is).
     The same ciphertexts with beta negated instead, and an honest ballot alongside, too."""
     from electionguard.ballot import ElectionKey, EncryptedBallots, Manifest, Verifier
     G, K, qbar, man_o, eb, sel = residue_forgery_case()
