@@ -24,6 +24,7 @@ from __future__ import annotations
 import ctypes
 import math
 import secrets
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -98,6 +99,8 @@ def partial_decrypt_batch(group: GroupContext, secret: int, qbar: int, texts: np
 
 class DecryptingTrustee:
     """GPU-backed DecryptingTrusteeIF (one process per trustee, one GPU each)."""
+
+    accepts_arrays = True  # texts may be an (n, 2, 512) wire-form array (the gRPC server passes one)
 
     def __init__(self, group: GroupContext, keys: GuardianKeys, commitments: Dict[str, List[int]]):
         self.group = group
@@ -180,6 +183,16 @@ def verify_shares(group: GroupContext, qbar: int, Ki: Sequence[int], texts, M: S
     return ok.astype(bool)
 
 
+def _concurrently(fn, items) -> list:
+    """[fn(x) for x in items], the calls made from one thread each (the first exception is
+    raised after every call has returned)."""
+    items = list(items)
+    if len(items) <= 1:
+        return [fn(x) for x in items]
+    with ThreadPoolExecutor(max_workers=len(items)) as ex:
+        return list(ex.map(fn, items))
+
+
 def lagrange(xs: Sequence[int], xi: int, q: int) -> int:
     num, den = 1, 1
     for xj in xs:
@@ -260,8 +273,12 @@ class Decryption:
         xs = [t.xCoordinate() for t in self.trustees]
         rec = DecryptionRecord(T, {t.id(): t.xCoordinate() for t in self.trustees}, {}, {}, [])
         parts = []  # (n,512) arrays to multiply together
-        for tr in self.trustees:
-            res = tr.directDecrypt(G, T, self.qbar)
+        # every trustee's batch is requested at once (remote trustees are separate processes,
+        # one GPU each); the checks and the combine below run in trustee order
+        direct = _concurrently(lambda tr: tr.directDecrypt(G, T, self.qbar), self.trustees)
+        pairs = [(l, tr) for l in self.missing for tr in self.trustees]
+        comp = iter(_concurrently(lambda lt: lt[1].compensatedDecrypt(G, lt[0], T, self.qbar), pairs))
+        for tr, res in zip(self.trustees, direct):
             if len(res) != n:  # remote proxies return [] on failure (RemoteDecryptingTrusteeProxy.java:64-66)
                 raise ValueError(f"trustee {tr.id()} returned {len(res)} of {n} direct decryptions")
             ok = verify_shares(G, self.qbar, [tr.electionPublicKey()] * n, T, [r.partialDecryption for r in res],
@@ -273,7 +290,7 @@ class Decryption:
         for l in self.missing:
             rec.compensated[l] = {}
             for tr in self.trustees:
-                res = tr.compensatedDecrypt(G, l, T, self.qbar)
+                res = next(comp)
                 if len(res) != n:
                     raise ValueError(f"trustee {tr.id()} returned {len(res)} of {n} compensated decryptions for {l}")
                 ok = verify_shares(G, self.qbar, [r.recoveredPublicKeyShare for r in res], T,

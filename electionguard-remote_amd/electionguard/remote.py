@@ -20,6 +20,7 @@ import threading
 from concurrent import futures
 from typing import List, Optional, Sequence
 
+import numpy as np
 from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
 
 log = logging.getLogger(__name__)
@@ -112,12 +113,20 @@ def publish_ct(pad: int, data: int):
     return MSG["ElGamalCiphertext"](pad=publish_p(pad), data=publish_p(data))
 
 
-def _texts_from(req):
-    out = []
-    for t in req.text:
+def _p_wire(m) -> bytes:
+    """An ElementModP's value as 512 big-endian bytes (new BigInteger(1, bytes), any length)."""
+    b = m.value
+    return b if len(b) == 512 else int.from_bytes(b, "big").to_bytes(512, "big")
+
+
+def _texts_from(req) -> np.ndarray:
+    """The request's ciphertexts as an (n, 2, 512) array, straight from the wire bytes."""
+    out = np.empty((len(req.text), 2, 512), dtype=np.uint8)
+    for i, t in enumerate(req.text):
         if not t.HasField("pad"):
             raise ValueError("ciphertext without pad")  # importCiphertext returns null (:60-62)
-        out.append((import_int(t.pad), import_int(t.data)))
+        out[i, 0] = np.frombuffer(_p_wire(t.pad), dtype=np.uint8)
+        out[i, 1] = np.frombuffer(_p_wire(t.data), dtype=np.uint8)
     return out
 
 
@@ -157,17 +166,26 @@ class DecryptingTrusteeServer:
     def stop(self) -> None:
         self.server.stop(grace=1).wait()
 
+    def _texts(self, req):
+        """(n, 2, 512) array for trustees that take one (DecryptingTrustee.accepts_arrays), else
+        (pad, data) int pairs as the reference's importCiphertext gives them."""
+        T = _texts_from(req)
+        if getattr(self.trustee, "accepts_arrays", False):
+            return T
+        return [(int.from_bytes(t[0].tobytes(), "big"), int.from_bytes(t[1].tobytes(), "big")) for t in T]
+
     # RunRemoteDecryptingTrustee.directDecrypt (:180-208)
     def _direct(self, req, ctx):
         resp = MSG["DirectDecryptionResponse"]()
         try:
-            texts = _texts_from(req)
+            texts = self._texts(req)
             qbar = import_int(req.extended_base_hash)
             res = self.trustee.directDecrypt(self.group, texts, qbar, None)
-            for r in res:
-                resp.results.add(decryption=publish_p(r.partialDecryption),
-                                 proof=MSG["GenericChaumPedersenProof"](challenge=publish_q(r.proof.c),
-                                                                        response=publish_q(r.proof.v)))
+            for r in res:  # field by field: a third of the cost of nested message constructors
+                x = resp.results.add()
+                x.decryption.value = int(r.partialDecryption).to_bytes(512, "big")
+                x.proof.challenge.value = int(r.proof.c).to_bytes(32, "big")
+                x.proof.response.value = int(r.proof.v).to_bytes(32, "big")
         except Exception as e:  # error string, not a gRPC status (:200-204)
             log.exception("directDecrypt failed")
             del resp.results[:]
@@ -178,14 +196,15 @@ class DecryptingTrusteeServer:
     def _compensated(self, req, ctx):
         resp = MSG["CompensatedDecryptionResponse"]()
         try:
-            texts = _texts_from(req)
+            texts = self._texts(req)
             qbar = import_int(req.extended_base_hash)
             res = self.trustee.compensatedDecrypt(self.group, req.missing_guardian_id, texts, qbar, None)
             for r in res:
-                resp.results.add(decryption=publish_p(r.partialDecryption),
-                                 proof=MSG["GenericChaumPedersenProof"](challenge=publish_q(r.proof.c),
-                                                                        response=publish_q(r.proof.v)),
-                                 recoveryPublicKey=publish_p(r.recoveredPublicKeyShare))
+                x = resp.results.add()
+                x.decryption.value = int(r.partialDecryption).to_bytes(512, "big")
+                x.proof.challenge.value = int(r.proof.c).to_bytes(32, "big")
+                x.proof.response.value = int(r.proof.v).to_bytes(32, "big")
+                x.recoveryPublicKey.value = int(r.recoveredPublicKeyShare).to_bytes(512, "big")
         except Exception as e:
             log.exception("compensatedDecrypt failed")
             del resp.results[:]
@@ -234,13 +253,19 @@ class RemoteDecryptingTrusteeProxy:
     def electionPublicKey(self) -> int:
         return self._K
 
-    def _batches(self, texts):
+    def _requests(self, make, texts):
+        """Consecutive requests of at most max_texts ciphertexts each, filled from the texts'
+        512-byte wire form (the bytes publish_ct writes)."""
         from .decrypt import _texts_array
 
         T = _texts_array(texts)
         for a in range(0, len(T), self.max_texts):
-            yield [publish_ct(int.from_bytes(t[0].tobytes(), "big"), int.from_bytes(t[1].tobytes(), "big"))
-                   for t in T[a:a + self.max_texts]]
+            req = make()
+            for t in T[a:a + self.max_texts]:
+                x = req.text.add()
+                x.pad.value = t[0].tobytes()
+                x.data.value = t[1].tobytes()
+            yield req
 
     def _call(self, name, stub, requests):
         import grpc
@@ -265,8 +290,8 @@ class RemoteDecryptingTrusteeProxy:
     def directDecrypt(self, group, texts, extendedBaseHash: int, nonce=None):
         from .decrypt import DirectDecryptionAndProof, GenericChaumPedersenProof
 
-        reqs = (MSG["DirectDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash), text=b)
-                for b in self._batches(texts))
+        reqs = self._requests(lambda: MSG["DirectDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash)),
+                              texts)
         res = self._call("directDecrypt", self._direct, reqs)
         if res is None:
             return []
@@ -278,9 +303,8 @@ class RemoteDecryptingTrusteeProxy:
     def compensatedDecrypt(self, group, missingGuardianId: str, texts, extendedBaseHash: int, nonce=None):
         from .decrypt import CompensatedDecryptionAndProof, GenericChaumPedersenProof
 
-        reqs = (MSG["CompensatedDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash),
-                                                     missing_guardian_id=missingGuardianId, text=b)
-                for b in self._batches(texts))
+        reqs = self._requests(lambda: MSG["CompensatedDecryptionRequest"](
+            extended_base_hash=publish_q(extendedBaseHash), missing_guardian_id=missingGuardianId), texts)
         res = self._call("compensatedDecrypt", self._comp, reqs)
         if res is None:
             return []
