@@ -38,20 +38,18 @@ def as_p_array(elems: Union[np.ndarray, Sequence["ElementModP"], Sequence[int]])
     if isinstance(elems, np.ndarray):
         a = np.ascontiguousarray(elems, dtype=np.uint8)
         return a.reshape(-1, P_BYTES)
-    out = np.empty((len(elems), P_BYTES), dtype=np.uint8)
-    for i, e in enumerate(elems):
-        out[i] = np.frombuffer(e.byteArray() if isinstance(e, ElementModP) else p_bytes(e), dtype=np.uint8)
-    return out
+    raw = bytearray().join(e.byteArray() if isinstance(e, ElementModP) else int(e).to_bytes(P_BYTES, "big")
+                           for e in elems)
+    return np.frombuffer(raw, dtype=np.uint8).reshape(-1, P_BYTES)
 
 
 def as_q_array(elems: Union[np.ndarray, Sequence["ElementModQ"], Sequence[int]]) -> np.ndarray:
     if isinstance(elems, np.ndarray):
         a = np.ascontiguousarray(elems, dtype=np.uint8)
         return a.reshape(-1, Q_BYTES)
-    out = np.empty((len(elems), Q_BYTES), dtype=np.uint8)
-    for i, e in enumerate(elems):
-        out[i] = np.frombuffer(e.byteArray() if isinstance(e, ElementModQ) else q_bytes(e), dtype=np.uint8)
-    return out
+    raw = bytearray().join(e.byteArray() if isinstance(e, ElementModQ) else int(e).to_bytes(Q_BYTES, "big")
+                           for e in elems)
+    return np.frombuffer(raw, dtype=np.uint8).reshape(-1, Q_BYTES)
 
 
 def _ptr(a: np.ndarray):

@@ -31,7 +31,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from .core import native
-from .core.group import GroupContext, as_p_array, p_bytes, q_bytes
+from .core.group import GroupContext, as_p_array, as_q_array, p_bytes, q_bytes
 from .keyceremony import GuardianKeys, backup_label, backup_open, poly_eval
 
 
@@ -173,9 +173,8 @@ def verify_shares(group: GroupContext, qbar: int, Ki: Sequence[int], texts, M: S
         K = as_p_array(list(Ki))
         Mm = as_p_array(list(M))
         pr = np.empty((n, 2, 32), dtype=np.uint8)
-        for i, p in enumerate(proofs):
-            pr[i, 0] = np.frombuffer(q_bytes(p.c), dtype=np.uint8)
-            pr[i, 1] = np.frombuffer(q_bytes(p.v), dtype=np.uint8)
+        pr[:, 0] = as_q_array([p.c for p in proofs])
+        pr[:, 1] = as_q_array([p.v for p in proofs])
         qb = q_bytes(qbar)
         native.check(group._lib, "eg_verify_shares",
                      group._lib.eg_verify_shares(group.handle, native.buf(qb), _ptr(K), _ptr(T), _ptr(Mm), _ptr(pr),
