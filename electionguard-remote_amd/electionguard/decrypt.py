@@ -124,6 +124,22 @@ class DecryptingTrustee:
         return [DirectDecryptionAndProof(_be_int(M[i]), GenericChaumPedersenProof(_be_int(pr[i, 0]), _be_int(pr[i, 1])))
                 for i in range(len(T))]
 
+    # Array forms for the gRPC server (remote.DecryptingTrusteeServer): the same shares and proofs
+    # as directDecrypt / compensatedDecrypt, kept in their wire bytes.
+    def directDecryptArrays(self, group: GroupContext, texts, extendedBaseHash: int, nonce=None):
+        """-> (M (n, 512), proofs (n, 2, 32)) uint8."""
+        T = _texts_array(texts)
+        return partial_decrypt_batch(group, self.keys.secret, extendedBaseHash, T, _nonces(group, len(T), nonce))
+
+    def compensatedDecryptArrays(self, group: GroupContext, missingGuardianId: str, texts, extendedBaseHash: int,
+                                 nonce=None):
+        """-> (M (n, 512), proofs (n, 2, 32), recovery key (512,)) uint8."""
+        share = self.share_of(missingGuardianId)
+        T = _texts_array(texts)
+        M, pr = partial_decrypt_batch(group, share, extendedBaseHash, T, _nonces(group, len(T), nonce))
+        rk = np.frombuffer(p_bytes(self.recovery_public_key(missingGuardianId)), dtype=np.uint8)
+        return M, pr, rk
+
     def recovery_public_key(self, missing_id: str) -> int:
         """g^{P_l(x_i)} = prod_j K_{l,j}^{x_i^j} (GPU powP batch + product)."""
         comm = self.commitments[missing_id]

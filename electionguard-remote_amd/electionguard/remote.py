@@ -180,6 +180,14 @@ class DecryptingTrusteeServer:
         try:
             texts = self._texts(req)
             qbar = import_int(req.extended_base_hash)
+            if hasattr(self.trustee, "directDecryptArrays"):  # shares straight from the GPU's bytes
+                M, pr = self.trustee.directDecryptArrays(self.group, texts, qbar, None)
+                for i in range(len(M)):
+                    x = resp.results.add()
+                    x.decryption.value = M[i].tobytes()
+                    x.proof.challenge.value = pr[i, 0].tobytes()
+                    x.proof.response.value = pr[i, 1].tobytes()
+                return resp
             res = self.trustee.directDecrypt(self.group, texts, qbar, None)
             for r in res:  # field by field: a third of the cost of nested message constructors
                 x = resp.results.add()
@@ -198,6 +206,17 @@ class DecryptingTrusteeServer:
         try:
             texts = self._texts(req)
             qbar = import_int(req.extended_base_hash)
+            if hasattr(self.trustee, "compensatedDecryptArrays"):
+                M, pr, rk = self.trustee.compensatedDecryptArrays(self.group, req.missing_guardian_id, texts, qbar,
+                                                                  None)
+                rkb = rk.tobytes()
+                for i in range(len(M)):
+                    x = resp.results.add()
+                    x.decryption.value = M[i].tobytes()
+                    x.proof.challenge.value = pr[i, 0].tobytes()
+                    x.proof.response.value = pr[i, 1].tobytes()
+                    x.recoveryPublicKey.value = rkb
+                return resp
             res = self.trustee.compensatedDecrypt(self.group, req.missing_guardian_id, texts, qbar, None)
             for r in res:
                 x = resp.results.add()
