@@ -205,8 +205,9 @@ int eg_verify_shares(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], const uint8
  * once; a dispatcher thread runs the batch as one eg_powp_batch / eg_fb_pow_batch (g) /
  * eg_multp_batch once the GPU is free and the oldest element has waited window_us, or when
  * max_batch elements are queued.  The caller's out must stay valid until eg_ticket_wait, which
- * blocks until the result is in out, frees the ticket and returns the batch's status.  Wait for
- * every ticket before eg_ctx_destroy (destroy first runs the queued elements).
+ * blocks until the result is in out, frees the ticket and returns the batch's status.
+ * eg_ctx_destroy first runs every queued element, and a ticket stays waitable after it (each
+ * ticket must still be waited once, to free it); submits racing destroy fail with EG_ERR_STATE.
  * eg_*_one = submit + wait.  Defaults: max_batch 16384, window 100 us. */
 typedef struct eg_ticket eg_ticket;
 int eg_ctx_set_coalescing(eg_ctx* ctx, size_t max_batch, uint32_t window_us);
