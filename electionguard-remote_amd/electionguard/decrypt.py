@@ -24,6 +24,7 @@ from __future__ import annotations
 import ctypes
 import math
 import secrets
+from collections.abc import Sequence as _SequenceABC
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -52,6 +53,115 @@ class CompensatedDecryptionAndProof:
     partialDecryption: int
     proof: GenericChaumPedersenProof
     recoveredPublicKeyShare: int
+
+
+class _ShareView:
+    """Share i of a ShareBatch: the fields of Direct/CompensatedDecryptionAndProof, read from and
+    written to the batch's arrays."""
+    __slots__ = ("_b", "_i")
+
+    def __init__(self, b: "ShareBatch", i: int):
+        self._b, self._i = b, i
+
+    @property
+    def partialDecryption(self) -> int:
+        return int.from_bytes(self._b.M[self._i].tobytes(), "big")
+
+    @partialDecryption.setter
+    def partialDecryption(self, v: int) -> None:
+        self._b.M[self._i] = np.frombuffer(p_bytes(v), dtype=np.uint8)
+
+    @property
+    def proof(self) -> GenericChaumPedersenProof:
+        pr = self._b.proofs[self._i]
+        return GenericChaumPedersenProof(int.from_bytes(pr[0].tobytes(), "big"), int.from_bytes(pr[1].tobytes(), "big"))
+
+    @proof.setter
+    def proof(self, p: GenericChaumPedersenProof) -> None:
+        self._b.proofs[self._i, 0] = np.frombuffer(q_bytes(p.c), dtype=np.uint8)
+        self._b.proofs[self._i, 1] = np.frombuffer(q_bytes(p.v), dtype=np.uint8)
+
+    @property
+    def recoveredPublicKeyShare(self) -> int:
+        if self._b.recovery is None:
+            raise AttributeError("a direct share has no recovery key")
+        return int.from_bytes(self._b.recovery[self._i].tobytes(), "big")
+
+    @recoveredPublicKeyShare.setter
+    def recoveredPublicKeyShare(self, v: int) -> None:
+        self._b.recovery[self._i] = np.frombuffer(p_bytes(v), dtype=np.uint8)
+
+    def _fields(self):
+        f = (self.partialDecryption, self.proof)
+        return f + (self.recoveredPublicKeyShare,) if self._b.recovery is not None else f
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, _ShareView):
+            return self._fields() == other._fields()
+        if isinstance(other, (DirectDecryptionAndProof, CompensatedDecryptionAndProof)):
+            return self._fields() == tuple(getattr(other, k) for k in (
+                ("partialDecryption", "proof", "recoveredPublicKeyShare") if self._b.recovery is not None
+                else ("partialDecryption", "proof")))
+        return NotImplemented
+
+    def __repr__(self) -> str:
+        return f"ShareView({self._fields()!r})"
+
+
+class ShareBatch(_SequenceABC):
+    """The n shares one trustee returns for a batch of texts, kept in their wire form: M (n, 512),
+    proofs (n, 2, 32) = (c, v) and, for compensated shares, the recovery keys (n, 512).  It is the
+    list DecryptingTrusteeIF.directDecrypt / compensatedDecrypt return (indexing yields share
+    objects whose fields read and write the arrays), and the mediator and the record checks take
+    the arrays directly (share_arrays), with no per-share conversion."""
+
+    def __init__(self, M: np.ndarray, proofs: np.ndarray, recovery: Optional[np.ndarray] = None):
+        self.M = np.ascontiguousarray(M, dtype=np.uint8).reshape(-1, 512)
+        self.proofs = np.ascontiguousarray(proofs, dtype=np.uint8).reshape(-1, 2, 32)
+        self.recovery = None if recovery is None else np.ascontiguousarray(recovery, dtype=np.uint8).reshape(-1, 512)
+
+    def __len__(self) -> int:
+        return len(self.M)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return ShareBatch(self.M[i], self.proofs[i], None if self.recovery is None else self.recovery[i])
+        n = len(self.M)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("share index out of range")
+        return _ShareView(self, i)
+
+    def __setitem__(self, i: int, share) -> None:
+        v = self[i]
+        v.partialDecryption = share.partialDecryption
+        v.proof = share.proof
+        if self.recovery is not None:
+            v.recoveredPublicKeyShare = share.recoveredPublicKeyShare
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, ShareBatch):
+            return (np.array_equal(self.M, other.M) and np.array_equal(self.proofs, other.proofs) and
+                    (self.recovery is None) == (other.recovery is None) and
+                    (self.recovery is None or np.array_equal(self.recovery, other.recovery)))
+        if isinstance(other, (list, tuple)):
+            return len(self) == len(other) and all(a == b for a, b in zip(self, other))
+        return NotImplemented
+
+
+def share_arrays(res) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray]]:
+    """(M (n, 512), proofs (n, 2, 32), recovery keys (n, 512) or None) of a trustee's result: the
+    arrays of a ShareBatch, or packed from a list of share objects."""
+    if isinstance(res, ShareBatch):
+        return res.M, res.proofs, res.recovery
+    res = list(res)
+    pr = np.empty((len(res), 2, 32), dtype=np.uint8)
+    pr[:, 0] = as_q_array([r.proof.c for r in res])
+    pr[:, 1] = as_q_array([r.proof.v for r in res])
+    rk = (as_p_array([r.recoveredPublicKeyShare for r in res])
+          if res and hasattr(res[0], "recoveredPublicKeyShare") else None)
+    return as_p_array([r.partialDecryption for r in res]), pr, rk
 
 
 def _ptr(a: np.ndarray):
@@ -118,11 +228,9 @@ class DecryptingTrustee:
         return self.keys.public_key
 
     def directDecrypt(self, group: GroupContext, texts, extendedBaseHash: int,
-                      nonce: Optional[Sequence[int]] = None) -> List[DirectDecryptionAndProof]:
-        T = _texts_array(texts)
-        M, pr = partial_decrypt_batch(group, self.keys.secret, extendedBaseHash, T, _nonces(group, len(T), nonce))
-        return [DirectDecryptionAndProof(_be_int(M[i]), GenericChaumPedersenProof(_be_int(pr[i, 0]), _be_int(pr[i, 1])))
-                for i in range(len(T))]
+                      nonce: Optional[Sequence[int]] = None) -> ShareBatch:
+        """-> the n DirectDecryptionAndProof, in text order (a ShareBatch)."""
+        return ShareBatch(*self.directDecryptArrays(group, texts, extendedBaseHash, nonce))
 
     # Array forms for the gRPC server (remote.DecryptingTrusteeServer): the same shares and proofs
     # as directDecrypt / compensatedDecrypt, kept in their wire bytes.
@@ -169,28 +277,33 @@ class DecryptingTrustee:
         return share
 
     def compensatedDecrypt(self, group: GroupContext, missingGuardianId: str, texts, extendedBaseHash: int,
-                           nonce: Optional[Sequence[int]] = None) -> List[CompensatedDecryptionAndProof]:
-        share = self.share_of(missingGuardianId)
-        T = _texts_array(texts)
-        M, pr = partial_decrypt_batch(group, share, extendedBaseHash, T, _nonces(group, len(T), nonce))
-        rk = self.recovery_public_key(missingGuardianId)
-        return [CompensatedDecryptionAndProof(_be_int(M[i]),
-                                              GenericChaumPedersenProof(_be_int(pr[i, 0]), _be_int(pr[i, 1])), rk)
-                for i in range(len(T))]
+                           nonce: Optional[Sequence[int]] = None) -> ShareBatch:
+        """-> the n CompensatedDecryptionAndProof, in text order (a ShareBatch)."""
+        M, pr, rk = self.compensatedDecryptArrays(group, missingGuardianId, texts, extendedBaseHash, nonce)
+        return ShareBatch(M, pr, np.tile(rk, (len(M), 1)))
 
 
-def verify_shares(group: GroupContext, qbar: int, Ki: Sequence[int], texts, M: Sequence[int],
-                  proofs: Sequence[GenericChaumPedersenProof]) -> np.ndarray:
-    """a = g^v K_i^c, b = pad^v M^c; c == H(qbar, pad, data, a, b, M).  -> bool (n,)"""
+def verify_shares(group: GroupContext, qbar: int, Ki, texts, M, proofs) -> np.ndarray:
+    """a = g^v K_i^c, b = pad^v M^c; c == H(qbar, pad, data, a, b, M).  -> bool (n,)
+    Ki: one key (int) for every share or one per share; M: ints or an (n, 512) array; proofs:
+    GenericChaumPedersenProof objects or an (n, 2, 32) array of (c, v)."""
     T = _texts_array(texts)
     n = len(T)
     ok = np.zeros(n, dtype=np.uint8)
     if n:
-        K = as_p_array(list(Ki))
-        Mm = as_p_array(list(M))
-        pr = np.empty((n, 2, 32), dtype=np.uint8)
-        pr[:, 0] = as_q_array([p.c for p in proofs])
-        pr[:, 1] = as_q_array([p.v for p in proofs])
+        if isinstance(Ki, (int, np.integer)):
+            K = np.ascontiguousarray(np.broadcast_to(np.frombuffer(p_bytes(Ki), dtype=np.uint8), (n, 512)))
+        else:
+            K = as_p_array(Ki if isinstance(Ki, np.ndarray) else list(Ki))
+        Mm = as_p_array(M if isinstance(M, np.ndarray) else list(M))
+        if isinstance(proofs, np.ndarray):
+            pr = np.ascontiguousarray(proofs, dtype=np.uint8).reshape(-1, 2, 32)
+        else:
+            pr = np.empty((n, 2, 32), dtype=np.uint8)
+            pr[:, 0] = as_q_array([p.c for p in proofs])
+            pr[:, 1] = as_q_array([p.v for p in proofs])
+        if len(K) != n or len(Mm) != n or len(pr) != n:
+            raise ValueError("verify_shares: keys, shares and proofs must match the texts")
         qb = q_bytes(qbar)
         native.check(group._lib, "eg_verify_shares",
                      group._lib.eg_verify_shares(group.handle, native.buf(qb), _ptr(K), _ptr(T), _ptr(Mm), _ptr(pr),
@@ -296,25 +409,24 @@ class Decryption:
         for tr, res in zip(self.trustees, direct):
             if len(res) != n:  # remote proxies return [] on failure (RemoteDecryptingTrusteeProxy.java:64-66)
                 raise ValueError(f"trustee {tr.id()} returned {len(res)} of {n} direct decryptions")
-            ok = verify_shares(G, self.qbar, [tr.electionPublicKey()] * n, T, [r.partialDecryption for r in res],
-                               [r.proof for r in res])
+            Md, prd, _ = share_arrays(res)
+            ok = verify_shares(G, self.qbar, tr.electionPublicKey(), T, Md, prd)
             if not ok.all():
                 raise ValueError(f"invalid direct decryption proof from {tr.id()}")
             rec.direct[tr.id()] = res
-            parts.append(as_p_array([r.partialDecryption for r in res]))
+            parts.append(Md)
         for l in self.missing:
             rec.compensated[l] = {}
             for tr in self.trustees:
                 res = next(comp)
                 if len(res) != n:
                     raise ValueError(f"trustee {tr.id()} returned {len(res)} of {n} compensated decryptions for {l}")
-                ok = verify_shares(G, self.qbar, [r.recoveredPublicKeyShare for r in res], T,
-                                   [r.partialDecryption for r in res], [r.proof for r in res])
+                Ml, prl, rkl = share_arrays(res)
+                ok = verify_shares(G, self.qbar, rkl, T, Ml, prl)
                 if not ok.all():
                     raise ValueError(f"invalid compensated decryption proof from {tr.id()} for {l}")
                 rec.compensated[l][tr.id()] = res
                 w = lagrange(xs, tr.xCoordinate(), G.q)
-                Ml = as_p_array([r.partialDecryption for r in res])
                 parts.append(G.powP_batch(Ml, [w] * n))
         k = len(parts)
         stacked = np.ascontiguousarray(np.stack(parts, axis=1)).reshape(n * k, 512)
@@ -386,9 +498,11 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
         if gid not in public_keys or gid not in rec.xs:
             out["direct_proofs"] = out["quorum"] = False
             continue
-        out["direct_proofs"] &= len(res) == n and bool(
-            verify_shares(G, qbar, [public_keys[gid]] * n, T, [r.partialDecryption for r in res],
-                          [r.proof for r in res]).all())
+        if len(res) != n:
+            out["direct_proofs"] = False
+            continue
+        Md, prd, _ = share_arrays(res)
+        out["direct_proofs"] &= bool(verify_shares(G, qbar, public_keys[gid], T, Md, prd).all())
     if len(rec.counts) != n or any(
             c is None or not isinstance(c, (int, np.integer)) or c < 0 or (max_count is not None and c > max_count)
             for c in rec.counts):
@@ -406,10 +520,13 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
             x = rec.xs[gid]
             exps = [pow(x, j, G.q) for j in range(len(comm))]
             want = _be_int(G.prodP_groups(G.powP_batch(comm, exps), 1, len(comm))[0])
-            out["recovery_keys"] &= len(res) == n and all(r.recoveredPublicKeyShare == want for r in res)
-            out["compensated_proofs"] &= len(res) == n and bool(
-                verify_shares(G, qbar, [r.recoveredPublicKeyShare for r in res], T,
-                              [r.partialDecryption for r in res], [r.proof for r in res]).all())
+            if len(res) != n:
+                out["recovery_keys"] = out["compensated_proofs"] = False
+                continue
+            Ml, prl, rkl = share_arrays(res)
+            out["recovery_keys"] &= rkl is not None and bool(
+                (rkl == np.frombuffer(p_bytes(want), dtype=np.uint8)).all())
+            out["compensated_proofs"] &= rkl is not None and bool(verify_shares(G, qbar, rkl, T, Ml, prl).all())
     lengths_ok = all(len(rec.direct[g]) == n for g in avail) and all(
         len(res) == n for by in rec.compensated.values() for res in by.values())
     if not lengths_ok:
@@ -417,11 +534,11 @@ def verify_decryption_record(group: GroupContext, qbar: int, rec: DecryptionReco
     if not (out["quorum"] and out["tally"] and n):
         return out
     xs = [rec.xs[g] for g in avail]
-    parts = [as_p_array([r.partialDecryption for r in rec.direct[g]]) for g in avail]
+    parts = [share_arrays(rec.direct[g])[0] for g in avail]
     for l, by_avail in rec.compensated.items():
         for gid in avail:
             w = lagrange(xs, rec.xs[gid], G.q)
-            parts.append(G.powP_batch(as_p_array([r.partialDecryption for r in by_avail[gid]]), [w] * n))
+            parts.append(G.powP_batch(share_arrays(by_avail[gid])[0], [w] * n))
     k = len(parts)
     M = G.prodP_groups(np.ascontiguousarray(np.stack(parts, axis=1)).reshape(n * k, 512), n, k)
     lhs = G.multP_batch(M, G.gPowP_batch([int(c) for c in rec.counts]))

@@ -119,6 +119,30 @@ def _p_wire(m) -> bytes:
     return b if len(b) == 512 else int.from_bytes(b, "big").to_bytes(512, "big")
 
 
+def _q_wire(m) -> bytes:
+    b = m.value
+    return b if len(b) == 32 else int.from_bytes(b, "big").to_bytes(32, "big")
+
+
+def _share_wire(results, recovery: bool = False):
+    """(M (n, 512), proofs (n, 2, 32)[, recovery keys (n, 512)]) from response results; an empty
+    element (importElementModP's null) raises ValueError."""
+    def need(m, conv):
+        if len(m.value) == 0:
+            raise ValueError("result with an empty element")
+        return conv(m)
+
+    n = len(results)
+    M = np.frombuffer(bytearray().join(need(r.decryption, _p_wire) for r in results), dtype=np.uint8).reshape(n, 512)
+    pr = np.frombuffer(bytearray().join(need(r.proof.challenge, _q_wire) + need(r.proof.response, _q_wire)
+                                        for r in results), dtype=np.uint8).reshape(n, 2, 32)
+    if not recovery:
+        return M, pr
+    rk = np.frombuffer(bytearray().join(need(r.recoveryPublicKey, _p_wire) for r in results),
+                       dtype=np.uint8).reshape(n, 512)
+    return M, pr, rk
+
+
 def _texts_from(req) -> np.ndarray:
     """The request's ciphertexts as an (n, 2, 512) array, straight from the wire bytes."""
     out = np.empty((len(req.text), 2, 512), dtype=np.uint8)
@@ -307,30 +331,32 @@ class RemoteDecryptingTrusteeProxy:
         return results
 
     def directDecrypt(self, group, texts, extendedBaseHash: int, nonce=None):
-        from .decrypt import DirectDecryptionAndProof, GenericChaumPedersenProof
-
         reqs = self._requests(lambda: MSG["DirectDecryptionRequest"](extended_base_hash=publish_q(extendedBaseHash)),
                               texts)
         res = self._call("directDecrypt", self._direct, reqs)
         if res is None:
             return []
-        return [DirectDecryptionAndProof(import_int(r.decryption),
-                                         GenericChaumPedersenProof(import_int(r.proof.challenge),
-                                                                   import_int(r.proof.response)))
-                for r in res]
+        from .decrypt import ShareBatch
+
+        try:
+            return ShareBatch(*_share_wire(res))
+        except (ValueError, OverflowError) as e:  # an empty (null) or oversized element
+            log.error("directDecrypt: %s", e)
+            return []
 
     def compensatedDecrypt(self, group, missingGuardianId: str, texts, extendedBaseHash: int, nonce=None):
-        from .decrypt import CompensatedDecryptionAndProof, GenericChaumPedersenProof
-
         reqs = self._requests(lambda: MSG["CompensatedDecryptionRequest"](
             extended_base_hash=publish_q(extendedBaseHash), missing_guardian_id=missingGuardianId), texts)
         res = self._call("compensatedDecrypt", self._comp, reqs)
         if res is None:
             return []
-        return [CompensatedDecryptionAndProof(import_int(r.decryption),
-                                              GenericChaumPedersenProof(import_int(r.proof.challenge),
-                                                                        import_int(r.proof.response)),
-                                              import_int(r.recoveryPublicKey)) for r in res]
+        from .decrypt import ShareBatch
+
+        try:
+            return ShareBatch(*_share_wire(res, recovery=True))
+        except (ValueError, OverflowError) as e:
+            log.error("compensatedDecrypt: %s", e)
+            return []
 
     def finish(self, all_ok: bool) -> str:
         import grpc
