@@ -145,13 +145,13 @@ def _share_wire(results, recovery: bool = False):
 
 def _texts_from(req) -> np.ndarray:
     """The request's ciphertexts as an (n, 2, 512) array, straight from the wire bytes."""
-    out = np.empty((len(req.text), 2, 512), dtype=np.uint8)
-    for i, t in enumerate(req.text):
+    def ct(t) -> bytes:
         if not t.HasField("pad"):
             raise ValueError("ciphertext without pad")  # importCiphertext returns null (:60-62)
-        out[i, 0] = np.frombuffer(_p_wire(t.pad), dtype=np.uint8)
-        out[i, 1] = np.frombuffer(_p_wire(t.data), dtype=np.uint8)
-    return out
+        return _p_wire(t.pad) + _p_wire(t.data)
+
+    raw = bytearray().join(ct(t) for t in req.text)
+    return np.frombuffer(raw, dtype=np.uint8).reshape(-1, 2, 512)
 
 
 class DecryptingTrusteeServer:
