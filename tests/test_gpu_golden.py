@@ -5,7 +5,8 @@ import numpy as np
 import pytest
 
 import eg_oracle as O
-from test_oracle_golden import MODES, _arr, golden_ballot_arrays, h, load, residue_forgery_case
+from test_oracle_golden import (MODES, _arr, ballot_wire_arrays, golden_ballot_arrays, h, load,
+                                residue_forgery_case, twisted_pair_case)
 
 pytestmark = pytest.mark.gpu
 
@@ -96,3 +97,16 @@ def test_gpu_rejects_non_residue_alpha_with_matching_proofs(group):
     assert ok_s[1].all() and ok_c[1].all()
     assert not ok_s[2, 4] and ok_s[2].sum() == man.nsel - 1          # beta residue (the hash fails too)
     assert ok_c[2].tolist() == [True, False]                          # B = prod beta is not a residue
+
+
+def test_gpu_rejects_contest_whose_selections_are_invalid(group):
+    """Contest 0 holds two alphas times p - 1: A = prod alpha is a valid residue and the contest
+    proof verifies, but its selections are invalid, so the contest is rejected (the round-3
+    contest rule, k_contest_flags), as both oracles do."""
+    from electionguard.ballot import ElectionKey, EncryptedBallots, Manifest, Verifier
+    G, K, qbar, man_o, eb = twisted_pair_case()
+    man = Manifest(man_o.n_contests, man_o.n_selections, man_o.votes_allowed)
+    ok_s, ok_c, _ = Verifier(group, ElectionKey(group, K), qbar, man).verify(
+        EncryptedBallots(*ballot_wire_arrays(eb)), with_tally=False)
+    assert ok_s[0].tolist() == [i > 1 for i in range(man.nsel)]
+    assert ok_c[0].tolist() == [False, True]

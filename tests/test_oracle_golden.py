@@ -234,6 +234,45 @@ def test_c_oracle_rejects_non_residue_alpha():
     assert ok_c[0].tolist() == [False, True]
 
 
+def twisted_pair_case(seed=78):
+    """An honest ballot whose contest 0 has the alphas of its first two selections multiplied by
+    p - 1 (order 2): both selections are non-residues, but A = prod alpha is unchanged, so the
+    contest's own proof still verifies.  The contest is rejected with its selections."""
+    G = O.production_group()
+    rng = random.Random(seed)
+    gs, K = O.key_ceremony(G, 2, 2, rng)
+    qbar = rng.randrange(G.q)
+    man = O.Manifest(2, 2, 1)
+    eb = O.encrypt_ballot(G, K, qbar, man, O.ballot_plaintexts(man, rng), rng)
+    for i in (0, 1):
+        eb.cts[i] = O.Ciphertext(eb.cts[i].pad * (G.p - 1) % G.p, eb.cts[i].data)
+    return G, K, qbar, man, eb
+
+
+def ballot_wire_arrays(eb):
+    b = lambda x, n: np.frombuffer(int(x).to_bytes(n, "big"), np.uint8)
+    cts = np.stack([np.stack([b(ct.pad, 512), b(ct.data, 512)]) for ct in eb.cts])[None]
+    rp = np.stack([np.stack([b(v, 32) for v in (pr.c0, pr.v0, pr.c1, pr.v1)]) for pr in eb.proofs])[None]
+    cp = np.stack([np.stack([b(pr.c, 32), b(pr.v, 32)]) for pr in eb.contest_proofs])[None]
+    return cts, rp, cp
+
+
+def test_contest_with_two_invalid_selections_is_rejected_by_both_oracles():
+    from eg_oracle_c import COracle
+    G, K, qbar, man, eb = twisted_pair_case()
+    spc = man.sel_per_contest
+    A = G.prodP([ct.pad for ct in eb.cts[:spc]])
+    B = G.prodP([ct.data for ct in eb.cts[:spc]])
+    assert O.is_valid_residue(G, A) and O.is_valid_residue(G, B)     # the aggregate alone passes
+    assert O.verify_constant_proof(G, K, qbar, A, B, man.votes_allowed, eb.contest_proofs[0])
+    assert not O.verify_ballot(G, K, qbar, man, eb)
+    co = COracle(G.p, G.q, G.g)
+    co.set_key(K)
+    ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, spc, 1, 1, *ballot_wire_arrays(eb), tally=False)
+    assert ok_s[0].tolist() == [i > 1 for i in range(len(eb.cts))]
+    assert ok_c[0].tolist() == [False, True]
+
+
 # --------------------------------------------------------------------------------------
 # Spoiled ballots (RunRemoteDecryptor.java:264-269): cast-only tally and decryptBallot.
 # --------------------------------------------------------------------------------------
