@@ -551,30 +551,14 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   // Outer loop: one Montgomery multiply (or square) per trip, at a single inlined site; the
   // inner loop runs the program's loads, stores and digit spreads up to the next multiply.
   uint32_t pc = 0;
-  const uint32_t* fb_col = nullptr;  // CT: the fixed-base window column being scanned
-  uint32_t fb_h = 0, fb_d = 0;
   while (true) {
-    const uint32_t* ysrc = nullptr;  // nullptr: square
-    uint32_t kind = OP_END, arg = 0;
-    while (true) {
-      const uint32_t op = sched[pc++];
-      kind = op & ((1u << kOpShift) - 1u);
-      arg = op >> kOpShift;
-      if (kind == OP_END || kind == OP_SQR) break;
-      if (kind == OP_MUL_BASE) { ysrc = B; break; }
-      if (kind == OP_MUL_TBL) { ysrc = tbl + (size_t)arg * kW; break; }
-      if (kind == OP_MUL_WIN) {  // arg = w | o << 12
-        const uint32_t w = arg & 4095u;
-        const uint32_t byte = scalars[(size_t)J[1 + (arg >> 12)] * S.exp_bytes + (w >> 1)];
-        ysrc = tbl + (size_t)((w & 1) ? (byte & 15u) : (byte >> 4)) * kW;
-        break;
-      }
-      if (kind == OP_MUL_COMB) { ysrc = tbl + (size_t)dig[arg] * kW; break; }
-      if (kind == OP_MUL_GATHER) {
-        ysrc = P.ygat + ((size_t)(J[2] + (arg >> 2)) * (kCombH - 1) + (arg & 3u)) * kW;
-        break;
-      }
-      if (kind == OP_MUL_FB || kind == OP_LOAD_FB) {
+    uint32_t op = sched[pc++];
+    uint32_t kind = op & ((1u << kOpShift) - 1u), arg = op >> kOpShift;
+    // loads, stores and digit spreads up to the next multiply; the multiply kinds (OP_SQR ..
+    // OP_MUL_FB) leave this loop without passing through any handler that rewrites x, so the
+    // multiply site keeps x in the registers the handlers use (no copies on the hot path)
+    while (kind > kOpMulLast) {
+      if (kind == OP_LOAD_FB) {
         const FbTab& T = (arg >> 10) ? fb1 : fb0;
         const uint32_t kf = arg & 255u;
         const uint32_t d = be_digit(scalars + (size_t)J[5 + 2 * ((arg >> 9) & 1u) + ((arg >> 8) & 1u)] * 32, 32,
@@ -582,71 +566,90 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
         if constexpr (CT) {
           // secret scalar (encryption nonces, the vote): masked scan of the window's whole
           // column of 2^wbits entries (small tables only, eg_ctx_set_ct_encrypt)
-          fb_col = T.data + (size_t)(kf << T.wbits) * kW;
-          fb_h = T.wbits;
-          fb_d = d;
-          if (kind == OP_MUL_FB) { ysrc = fb_col; break; }
-          ct_select_to_lds(slot, fb_col, fb_h, fb_d);
+          ct_select_to_lds(slot, T.data + (size_t)(kf << T.wbits) * kW, T.wbits, d);
           wave_sync();
           load_elem(x, slot);
           wave_sync();
-          continue;
+        } else {
+          load_elem(x, T.data + ((size_t)(kf << T.wbits) + d) * kW);
         }
-        const uint32_t* ent = T.data + ((size_t)(kf << T.wbits) + d) * kW;
-        if (kind == OP_MUL_FB) { ysrc = ent; break; }
-        load_elem(x, ent);
-        continue;
-      }
-      switch (kind) {
-        case OP_LOAD_ONE: load_elem(x, C->one); break;
-        case OP_LOAD_BASE: load_elem(x, B); break;
-        case OP_LOAD_TBL: load_elem(x, tbl + (size_t)arg * kW); break;
-        case OP_LOAD_WIN: load_elem(x, tbl + (size_t)(scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4) * kW); break;
-        case OP_LOAD_COMB:
-          if constexpr (CT) {
-            ct_select_to_lds(slot, tbl, ch, dig[arg]);
-            wave_sync();
-            load_elem(x, slot);
-            wave_sync();
-          } else {
-            load_elem(x, tbl + (size_t)dig[arg] * kW);
-          }
-          break;
-        case OP_LOAD_GATHER: load_elem(x, P.ygat + ((size_t)J[2] * (kCombH - 1) + arg) * kW); break;
-        case OP_STORE_TBL: store_elem(tbl + (size_t)arg * kW, x); break;
-        case OP_STORE_Y:
-          if (P.yout != nullptr && live) store_elem(P.yout + ((size_t)gid * (kCombH - 1) + arg) * kW, x);
-          break;
-        case OP_STORE_R:
-          if (live) store_elem(P.rout + ((size_t)gid * 2 + arg) * kW, x);
-          break;
-        case OP_STORE_OUT:
-          if (live) store_elem(out + (size_t)J[3 + arg] * kW, x);
-          break;
-        case OP_EXP:
-          if (S.comb) {
-            // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each); with
-            // two column blocks, columns 26..51 index the second table (entry 32 + digit)
-            const uint8_t* e = scalars + (size_t)J[1 + arg] * 32;
-            const int cw = (int)comb_width(S.rows);
-            const int hi = S.blocks == 2 ? cw / 2 : cw;
-            wave_sync();
-            for (int j = glane(); j < cw; j += kT) {
-              uint32_t d = j >= hi ? (1u << ch) : 0u;
-#pragma unroll
-              for (int r = 0; r < kCombH; ++r) {
-                const int bit = r * cw + j;
-                if (r < (int)ch && bit < 256) d |= (((uint32_t)e[31 - (bit >> 3)] >> (bit & 7)) & 1u) << r;
-              }
-              dig[j] = (uint8_t)d;
+      } else {
+        switch (kind) {
+          case OP_LOAD_ONE: load_elem(x, C->one); break;
+          case OP_LOAD_BASE: load_elem(x, B); break;
+          case OP_LOAD_TBL: load_elem(x, tbl + (size_t)arg * kW); break;
+          case OP_LOAD_WIN: load_elem(x, tbl + (size_t)(scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4) * kW); break;
+          case OP_LOAD_COMB:
+            if constexpr (CT) {
+              ct_select_to_lds(slot, tbl, ch, dig[arg]);
+              wave_sync();
+              load_elem(x, slot);
+              wave_sync();
+            } else {
+              load_elem(x, tbl + (size_t)dig[arg] * kW);
             }
-            wave_sync();
-          }
-          break;
-        default: break;
+            break;
+          case OP_LOAD_GATHER: load_elem(x, P.ygat + ((size_t)J[2] * (kCombH - 1) + arg) * kW); break;
+          case OP_STORE_TBL: store_elem(tbl + (size_t)arg * kW, x); break;
+          case OP_STORE_Y:
+            if (P.yout != nullptr && live) store_elem(P.yout + ((size_t)gid * (kCombH - 1) + arg) * kW, x);
+            break;
+          case OP_STORE_R:
+            if (live) store_elem(P.rout + ((size_t)gid * 2 + arg) * kW, x);
+            break;
+          case OP_STORE_OUT:
+            if (live) store_elem(out + (size_t)J[3 + arg] * kW, x);
+            break;
+          case OP_EXP:
+            if (S.comb) {
+              // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each); with
+              // two column blocks, columns 26..51 index the second table (entry 32 + digit)
+              const uint8_t* e = scalars + (size_t)J[1 + arg] * 32;
+              const int cw = (int)comb_width(S.rows);
+              const int hi = S.blocks == 2 ? cw / 2 : cw;
+              wave_sync();
+              for (int j = glane(); j < cw; j += kT) {
+                uint32_t d = j >= hi ? (1u << ch) : 0u;
+#pragma unroll
+                for (int r = 0; r < kCombH; ++r) {
+                  const int bit = r * cw + j;
+                  if (r < (int)ch && bit < 256) d |= (((uint32_t)e[31 - (bit >> 3)] >> (bit & 7)) & 1u) << r;
+                }
+                dig[j] = (uint8_t)d;
+              }
+              wave_sync();
+            }
+            break;
+          default: break;
+        }
       }
+      op = sched[pc++];
+      kind = op & ((1u << kOpShift) - 1u);
+      arg = op >> kOpShift;
     }
     if (kind == OP_END) break;
+    // the multiply's operand: nullptr = square
+    const uint32_t* ysrc = nullptr;
+    const uint32_t* fb_col = nullptr;  // CT: the fixed-base window column the multiply scans
+    uint32_t fb_h = 0, fb_d = 0;
+    if (kind == OP_MUL_BASE) ysrc = B;
+    else if (kind == OP_MUL_TBL) ysrc = tbl + (size_t)arg * kW;
+    else if (kind == OP_MUL_WIN) {  // arg = w | o << 12
+      const uint32_t w = arg & 4095u;
+      const uint32_t byte = scalars[(size_t)J[1 + (arg >> 12)] * S.exp_bytes + (w >> 1)];
+      ysrc = tbl + (size_t)((w & 1) ? (byte & 15u) : (byte >> 4)) * kW;
+    } else if (kind == OP_MUL_COMB) ysrc = tbl + (size_t)dig[arg] * kW;
+    else if (kind == OP_MUL_GATHER) ysrc = P.ygat + ((size_t)(J[2] + (arg >> 2)) * (kCombH - 1) + (arg & 3u)) * kW;
+    else if (kind == OP_MUL_FB) {
+      const FbTab& T = (arg >> 10) ? fb1 : fb0;
+      const uint32_t kf = arg & 255u;
+      const uint32_t d = be_digit(scalars + (size_t)J[5 + 2 * ((arg >> 9) & 1u) + ((arg >> 8) & 1u)] * 32, 32,
+                                  kf * T.wbits, T.wbits);
+      fb_col = T.data + (size_t)(kf << T.wbits) * kW;
+      fb_h = T.wbits;
+      fb_d = d;
+      ysrc = fb_col + (CT ? 0 : (size_t)d * kW);
+    }
     // ---- the one Montgomery multiply (or square) ----
     if (ysrc) {
       if constexpr (CT) {

@@ -6,7 +6,8 @@
 #   base: the production kernel;
 #   x2:   -DEG_TRAFFIC_X2=1, whose comb multiplies also read a far job's table entry (an L2
 #         miss) into a discarded LDS word -- more HBM bytes per launch at a nearly equal VALU count;
-#   peel: any later source revision built the same way.
+#   peel, loop2, head: any other source revision built the same way (r03d: the peeled CIOS step;
+#         r03j: the op loop with the multiply kinds split from the handlers).
 # Rounds of bench runs (base, x2, ..., base, x2, ...) give ballots/s and the held clock; one
 # FETCH_SIZE, one WRITE_SIZE and one SQ pass per variant give HBM bytes and VALU instructions per
 # launch; tools/ab_traffic_summary.py folds them into one JSON.
