@@ -405,8 +405,9 @@ static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const
 // Run a homogeneous batch of exponentiation jobs (device job records).
 // yout (comb jobs, optional): y_1..y_4 of every job, (kCombH-1) device elements per job, kept for a
 // later gather launch; ygat: the y_k array a gather launch (S.gather > 0) multiplies together.
-// tail (optional): a second, independent job population (shape tail->S) appended to the LAST
-// sub-launch so its short jobs fill that launch's tail (PowPart in eg_kernels.hpp).
+// tail, tail2 (optional): up to two more independent job populations (shapes tail->S, tail2->S)
+// appended to the LAST sub-launch so their short jobs fill that launch's tail (PowPart in
+// eg_kernels.hpp).
 // jobs per k_pow sub-launch (bounds the per-launch scratch: 32 or 64 comb entries per job)
 constexpr size_t kPowMaxJobs = (size_t)1 << 18;
 
@@ -430,69 +431,80 @@ static size_t pow_scratch_per_group(const PowShape& S) {
 static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size_t njobs, const uint32_t* d_elems,
                       const uint8_t* d_scal, uint32_t* d_out, FbTab f0, FbTab f1, uint32_t* yout = nullptr,
                       const uint32_t* ygat = nullptr, const PowTail* tail = nullptr, uint32_t* rout = nullptr,
-                      bool ct = false, const uint32_t* ctab = nullptr, uint32_t* scratch = nullptr) {
+                      bool ct = false, const uint32_t* ctab = nullptr, uint32_t* scratch = nullptr,
+                      const PowTail* tail2 = nullptr) {
+  if (tail && !tail->njobs) tail = nullptr;
+  if (tail2 && !tail2->njobs) tail2 = nullptr;
+  if (tail2 && !tail) std::swap(tail, tail2);
   if (scratch && (tail || njobs > kPowMaxJobs || njobs > kGroupsPerBlock))
     return fail(EG_ERR_ARG, "an explicit k_pow scratch takes one workgroup of jobs and no tail");
-  if (S.resid && (!S.comb || S.gather || !rout)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
-  if (S.blocks > 1 && (S.blocks != 2 || !S.comb || S.gather || S.shared_comb))
-    return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
-  if (tail && tail->S.blocks > 1 && (tail->S.blocks != 2 || !tail->S.comb || tail->S.gather || tail->S.shared_comb))
-    return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
-  if (S.shared_comb && (!S.comb || S.gather || S.resid || !ctab)) return fail(EG_ERR_ARG, "shared comb table missing");
-  if ((S.rows && (S.rows != 4 || !S.comb || S.gather || S.shared_comb || S.resid)) ||
-      (tail && tail->S.rows))
-    return fail(EG_ERR_ARG, "4-row combs are plain comb shapes without residue pairs");
   // constant-time shapes: a comb (masked scans of its tables) without fixed-base terms, or
   // fixed-base terms alone from small-window tables (masked scans of 2^w-entry window columns)
   auto ct_shape = [&](const PowShape& X) {
     if (X.has_base) return X.comb && !X.gather && !X.nfb[0] && !X.nfb[1];
     return f0.wbits <= kCtMaxWindow && f1.wbits <= kCtMaxWindow;
   };
-  if (ct && (!ct_shape(S) || (tail && !ct_shape(tail->S))))
-    return fail(EG_ERR_ARG, "constant-time jobs are plain combs or small-window fixed-base terms");
-  if (tail && tail->S.shared_comb && (!tail->S.comb || tail->S.gather || tail->S.resid || !tail->ctab))
-    return fail(EG_ERR_ARG, "shared comb table missing");
-  if (S.gather && (!S.comb || !ygat)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
-  if (tail && tail->S.gather && (!tail->S.comb || !tail->ygat))
-    return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
-  if (tail && tail->S.resid && (!tail->S.comb || tail->S.gather || !tail->rout))
-    return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
-  if (tail && !tail->njobs) tail = nullptr;
+  // every population of the launch: its shape and the buffers it needs
+  auto check = [&](const PowShape& X, bool is_tail, const uint32_t* yg, const uint32_t* ro, const uint32_t* ct_tab) {
+    if (X.resid && (!X.comb || X.gather || !ro)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
+    if (X.blocks > 1 && (X.blocks != 2 || !X.comb || X.gather || X.shared_comb))
+      return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
+    if (X.shared_comb && (!X.comb || X.gather || X.resid || !ct_tab)) return fail(EG_ERR_ARG, "shared comb table missing");
+    if ((X.rows && is_tail) || (X.rows && (X.rows != 4 || !X.comb || X.gather || X.shared_comb || X.resid)))
+      return fail(EG_ERR_ARG, "4-row combs are plain comb shapes without residue pairs");
+    if (ct && !ct_shape(X)) return fail(EG_ERR_ARG, "constant-time jobs are plain combs or small-window fixed-base terms");
+    if (X.gather && (!X.comb || !yg)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
+    return (int)EG_OK;
+  };
+  int src = check(S, false, ygat, rout, ctab);
+  if (!src && tail) src = check(tail->S, true, tail->ygat, tail->rout, tail->ctab);
+  if (!src && tail2) src = check(tail2->S, true, tail2->ygat, tail2->rout, tail2->ctab);
+  if (src) return src;
   if (!njobs && !tail) return EG_OK;
   const size_t per = pow_scratch_per_group(S);
   const size_t per1 = tail ? pow_scratch_per_group(tail->S) : 0;
+  const size_t per2 = tail2 ? pow_scratch_per_group(tail2->S) : 0;
   // bound the per-launch scratch (table of 16/32 powers per job)
   const size_t max_jobs = kPowMaxJobs;
-  MMCount mm_job, mm_tail;
-  const uint32_t *sched = nullptr, *sched_tail = nullptr;
-  int src = pow_schedule_dev(c, S, f0, f1, &sched, &mm_job);
+  MMCount mm_job, mm_tail, mm_tail2;
+  const uint32_t *sched = nullptr, *sched_tail = nullptr, *sched_tail2 = nullptr;
+  src = pow_schedule_dev(c, S, f0, f1, &sched, &mm_job);
   if (!src && tail) src = pow_schedule_dev(c, tail->S, f0, f1, &sched_tail, &mm_tail);
+  if (!src && tail2) src = pow_schedule_dev(c, tail2->S, f0, f1, &sched_tail2, &mm_tail2);
   if (src) return src;
   size_t off = 0;
   do {
     const size_t nj = std::min(max_jobs, njobs - off);
     const bool last = off + nj >= njobs;
     const size_t nt = (last && tail) ? tail->njobs : 0;
+    const size_t nt2 = (last && tail2) ? tail2->njobs : 0;
     uint32_t* scr = scratch;
     if (!scr) {
-      const int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1, (void**)&scr);
+      const int rc = ws_get(c, W_SCR, padded_groups(nj) * per + padded_groups(nt) * per1 + padded_groups(nt2) * per2,
+                            (void**)&scr);
       if (rc) return rc;
     }
     PowPart P0{S, sched, d_jobs + off * kJobWords, (uint32_t)nj, grid_for(nj), scr,
                yout ? yout + off * (kCombH - 1) * kW : nullptr, ygat, rout ? rout + off * 2 * kW : nullptr, ctab};
-    PowPart P1{};
+    PowPart P1{}, P2{};
     if (nt) {
       P1 = PowPart{tail->S, sched_tail, tail->jobs, (uint32_t)nt, grid_for(nt),
                    scr + padded_groups(nj) * per / 4, tail->yout, tail->ygat, tail->rout, tail->ctab};
     }
-    const dim3 grid(P0.nblocks + P1.nblocks);
+    if (nt2) {
+      P2 = PowPart{tail2->S, sched_tail2, tail2->jobs, (uint32_t)nt2, grid_for(nt2),
+                   scr + (padded_groups(nj) * per + padded_groups(nt) * per1) / 4, tail2->yout, tail2->ygat,
+                   tail2->rout, tail2->ctab};
+    }
+    const dim3 grid(P0.nblocks + P1.nblocks + P2.nblocks);
     ProfRec* pr = nullptr;
     uint64_t* clk = nullptr;
     if (c->timing) {
       // the record joins the window before anything can fail, so profile_end / destroy free its events
       c->prof.push_back(ProfRec{nullptr, nullptr,
-                                (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt,
-                                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt});
+                                (mm_job.mul + mm_job.sqr) * (double)nj + (mm_tail.mul + mm_tail.sqr) * (double)nt +
+                                    (mm_tail2.mul + mm_tail2.sqr) * (double)nt2,
+                                mm_job.sqr * (double)nj + mm_tail.sqr * (double)nt + mm_tail2.sqr * (double)nt2});
       pr = &c->prof.back();
       HIPCHK(hipEventCreate(&pr->a));
       HIPCHK(hipEventCreate(&pr->b));
@@ -503,11 +515,11 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
       HIPCHK(hipEventRecord(pr->a, c->stream));
     }
     if (c->h.friendly) {
-      if (ct) hipLaunchKernelGGL((k_pow<true, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
-      else hipLaunchKernelGGL((k_pow<true, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
+      if (ct) hipLaunchKernelGGL((k_pow<true, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, P2, d_elems, d_scal, d_out, f0, f1, clk);
+      else hipLaunchKernelGGL((k_pow<true, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, P2, d_elems, d_scal, d_out, f0, f1, clk);
     } else {
-      if (ct) hipLaunchKernelGGL((k_pow<false, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
-      else hipLaunchKernelGGL((k_pow<false, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, d_elems, d_scal, d_out, f0, f1, clk);
+      if (ct) hipLaunchKernelGGL((k_pow<false, true>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, P2, d_elems, d_scal, d_out, f0, f1, clk);
+      else hipLaunchKernelGGL((k_pow<false, false>), grid, dim3(kBlock), 0, c->stream, c->d, P0, P1, P2, d_elems, d_scal, d_out, f0, f1, clk);
     }
     HIPCHK(hipGetLastError());
     if (pr) HIPCHK(hipEventRecord(pr->b, c->stream));

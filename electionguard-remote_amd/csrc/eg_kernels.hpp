@@ -491,10 +491,11 @@ __host__ __device__ constexpr uint32_t fb_arg(uint32_t o, uint32_t t, uint32_t t
   return kf | (t << 8) | (o << 9) | (tab << 10);
 }
 
-// One launch may carry two job populations of different shapes (e.g. the beta jobs and the
-// contest-A jobs that only depend on the previous launch): part 0 owns the first P0.nblocks
-// workgroups, part 1 the rest, so the short part-1 jobs fill the tail of part 0 instead of
-// running as a separate, under-filled launch.  The shape stays workgroup-uniform.
+// One launch may carry up to three job populations of different shapes (e.g. the beta jobs,
+// the contest-A jobs that only depend on the previous launch and the contest-B jobs whose
+// betas the previous launch finished): part 0 owns the first P0.nblocks workgroups, part 1 the
+// next P1.nblocks, part 2 the rest, so the short jobs of parts 1-2 fill the tail of part 0
+// instead of running as a separate, under-filled launch.  The shape stays workgroup-uniform.
 struct PowPart {
   PowShape S;
   const uint32_t* sched;  // the shape's op program (pow_schedule), OP_END-terminated
@@ -516,7 +517,7 @@ struct PowPart {
 // addresses depend on exponent bits.
 template <bool F, bool CT>
 __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowPart P0,
-                                                PowPart P1, const uint32_t* __restrict__ elems,
+                                                PowPart P1, PowPart P2, const uint32_t* __restrict__ elems,
                                                 const uint8_t* __restrict__ scalars,
                                                 uint32_t* __restrict__ out, FbTab fb0, FbTab fb1,
                                                 uint64_t* __restrict__ clk) {
@@ -525,15 +526,17 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   // ticks (s_memrealtime) from its start to its end; the host reports the median per-workgroup
   // ratio (eg_clock_median), the in-kernel clock of MI355X_MICROARCH.md 'DVFS give-back' item 6
   const uint64_t cyc0 = clk ? __builtin_amdgcn_s_memtime() : 0, wall0 = clk ? __builtin_amdgcn_s_memrealtime() : 0;
-  const bool second = blockIdx.x >= P0.nblocks;
-  const PowPart& P = second ? P1 : P0;  // kernarg memory: shape fields stay scalar loads
+  const uint32_t b01 = P0.nblocks + P1.nblocks;
+  const uint32_t part = blockIdx.x < P0.nblocks ? 0u : (blockIdx.x < b01 ? 1u : 2u);
+  // kernarg memory: shape fields stay scalar loads
+  const PowPart& P = part == 0 ? P0 : (part == 1 ? P1 : P2);
   const PowShape& S = P.S;
   // the op program is read-only for the kernel's lifetime: through the constant address space
   // its words are scalar loads (s_load), not vector loads plus readfirstlane
   typedef __attribute__((address_space(4))) const uint32_t const_u32;
   const const_u32* sched = (const const_u32*)P.sched;
   const uint32_t njobs = P.njobs;
-  const uint32_t gid0 = (blockIdx.x - (second ? P0.nblocks : 0u)) * kGroupsPerBlock;  // wave-uniform
+  const uint32_t gid0 = (blockIdx.x - (part == 0 ? 0u : (part == 1 ? P0.nblocks : b01))) * kGroupsPerBlock;  // wave-uniform
   uint32_t* slot = group_slot();
   uint8_t* dig = s_dig[threadIdx.x / kT];
   Mont<F> M;

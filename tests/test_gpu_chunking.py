@@ -253,7 +253,8 @@ def test_oversized_arguments_rejected(group):
 @pytest.mark.parametrize("slots", ["0", "37", "100", "768", "5000"])
 def test_launch_split_independent(group, slots, monkeypatch):
     """The verifier sizes its three k_pow launches from the resident-workgroup count (beta
-    head in launch 1, contest-a jobs split between launches 2 and 3; eg_capi_ballot.inc).
+    head in launch 1; every contest-a job and the contest-b jobs whose betas all ran in launch 1
+    in launch 2; the other contest-b jobs, at most one round, in launch 3; eg_capi_ballot.inc).
     Verdicts and tally must not depend on where the splits fall: EG_POW_SLOTS forces other
     split points (0 = no split), against the CPython tally and a tamper in the moved jobs."""
     from electionguard.ballot import EncryptedBallots, Manifest, Verifier
@@ -267,10 +268,11 @@ def test_launch_split_independent(group, slots, monkeypatch):
     assert np.array_equal(tally, _tally_products(man, eb))
     rp, cp = eb.rproof.copy(), eb.cproof.copy()
     rp[3, 7, 2, 4] ^= 0x08       # a beta-head job (ballot 3) in launch 1 when split
-    cp[650, 1, 1, 9] ^= 0x20     # a late contest-a job (launch 3 when split)
+    cp[10, 2, 1, 3] ^= 0x10      # an early contest (its contest-b job in launch 2 when split)
+    cp[650, 1, 1, 9] ^= 0x20     # a late contest (its contest-b job in launch 3 when split)
     ok_s, ok_c, _ = V.verify(EncryptedBallots(eb.cts, rp, cp), with_tally=False)
     assert np.argwhere(~ok_s).tolist() == [[3, 7]]
-    assert np.argwhere(~ok_c).tolist() == [[650, 1]]
+    assert np.argwhere(~ok_c).tolist() == [[10, 2], [650, 1]]
 
 
 def test_cast_mask_across_verify_chunks(group):

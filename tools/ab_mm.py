@@ -124,6 +124,8 @@ if __name__ == "__main__":
             env_extra["EG_NO_COMB"] = "1"
         if name.endswith("@notail"):
             env_extra["EG_TAIL_SPLIT"] = "0"
+        if name.endswith("@cbl3"):  # every contest-b job in launch 3 (the schedule before early contest b)
+            env_extra["EG_CB_EARLY"] = "0"
         lib = build(name.split("@")[0], flags)
         nb = int(os.environ.get("AB_NB", "4000"))
         if mode == "verify":
