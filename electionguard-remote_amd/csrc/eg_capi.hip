@@ -183,6 +183,7 @@ struct eg_ctx {
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
   // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
   size_t pow_slots = 0;
+  uint32_t pow_wps = 3;                 // k_pow waves per SIMD at that occupancy
   double prof_clock_ghz = 0;  // shader clock over the last profiled k_pow launches (eg_ctx_profile_clock)
   // fixed-base tables of guardian keys K_i for large share-proof batches (eg_verify_shares),
   // most recently used first
@@ -410,6 +411,9 @@ static int pow_schedule_dev(eg_ctx* c, const PowShape& S, const FbTab& f0, const
 // eg_kernels.hpp).
 // jobs per k_pow sub-launch (bounds the per-launch scratch: 32 or 64 comb entries per job)
 constexpr size_t kPowMaxJobs = (size_t)1 << 18;
+// jobs of a last sub-launch together with its tails that a caller may plan for (the verifier's
+// beta head in launch 1): bounds that launch's scratch to ~21 GB of 40-KB comb tables
+constexpr size_t kPowTailJobs = (size_t)1 << 19;
 
 struct PowTail {
   PowShape S;
@@ -689,7 +693,10 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     const char* ts = getenv("EG_TAIL_SPLIT");
     if (!(ts && ts[0] == '0') && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pow<true, false>, kBlock, 0) == hipSuccess)
+    {
       c->pow_slots = (size_t)cus * (size_t)per_cu;
+      c->pow_wps = (uint32_t)std::max(1, per_cu / 4);  // kBlock = one wave: 4 SIMDs per CU
+    }
   }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {

@@ -126,6 +126,8 @@ if __name__ == "__main__":
             env_extra["EG_TAIL_SPLIT"] = "0"
         if name.endswith("@cbl3"):  # every contest-b job in launch 3 (the schedule before early contest b)
             env_extra["EG_CB_EARLY"] = "0"
+        if "@l3w" in name:  # launch 3 sized to 1..3 waves per SIMD (default 2)
+            env_extra["EG_L3_WAVES"] = name.split("@l3w")[1][:1]
         lib = build(name.split("@")[0], flags)
         nb = int(os.environ.get("AB_NB", "4000"))
         if mode == "verify":
