@@ -250,8 +250,8 @@ def test_oversized_arguments_rejected(group):
     assert rc == 1 and b"manifest" in lib.eg_last_error()
 
 
-@pytest.mark.parametrize("slots", ["0", "37", "100", "768", "5000"])
-def test_launch_split_independent(group, slots, monkeypatch):
+@pytest.mark.parametrize("slots,l3w", [("0", "2"), ("37", "2"), ("37", "1"), ("100", "3"), ("768", "2"), ("5000", "2")])
+def test_launch_split_independent(group, slots, l3w, monkeypatch):
     """The verifier sizes its three k_pow launches from the resident-workgroup count (beta
     head in launch 1; every contest-a job and the contest-b jobs whose betas all ran in launch 1
     in launch 2; the other contest-b jobs, at most one round, in launch 3; eg_capi_ballot.inc).
@@ -263,6 +263,7 @@ def test_launch_split_independent(group, slots, monkeypatch):
     key, K, qbar, eb = _encrypt(group, man, nb, 91)
     V = Verifier(group, key, qbar, man)
     monkeypatch.setenv("EG_POW_SLOTS", slots)
+    monkeypatch.setenv("EG_L3_WAVES", l3w)  # launch 3's size in waves per SIMD
     ok_s, ok_c, tally = V.verify(eb)
     assert ok_s.all() and ok_c.all()
     assert np.array_equal(tally, _tally_products(man, eb))
