@@ -692,10 +692,10 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     int cus = 0, per_cu = 0;
     const char* ts = getenv("EG_TAIL_SPLIT");
     if (!(ts && ts[0] == '0') && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pow<true, false>, kBlock, 0) == hipSuccess)
-    {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_pow<true, false>, kBlock, 0) == hipSuccess && per_cu > 0) {
       c->pow_slots = (size_t)cus * (size_t)per_cu;
-      c->pow_wps = (uint32_t)std::max(1, per_cu / 4);  // kBlock = one wave: 4 SIMDs per CU
+      // waves per SIMD: per_cu workgroups of kBlock / 64 waves over a CU's 4 SIMDs (3 for k_pow)
+      c->pow_wps = (uint32_t)std::max(1, per_cu * (kBlock / 64) / 4);
     }
   }
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

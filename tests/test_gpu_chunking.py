@@ -250,20 +250,24 @@ def test_oversized_arguments_rejected(group):
     assert rc == 1 and b"manifest" in lib.eg_last_error()
 
 
-@pytest.mark.parametrize("slots,l3w", [("0", "2"), ("37", "2"), ("37", "1"), ("100", "3"), ("768", "2"), ("5000", "2")])
-def test_launch_split_independent(group, slots, l3w, monkeypatch):
+@pytest.mark.parametrize("slots,cbe,l3w", [("0", "0", "2"), ("37", "0", "2"), ("100", "0", "2"), ("768", "0", "2"),
+                                           ("5000", "0", "2"), ("37", "1", "2"), ("37", "1", "1"), ("100", "1", "3"),
+                                           ("768", "1", "2")])
+def test_launch_split_independent(group, slots, cbe, l3w, monkeypatch):
     """The verifier sizes its three k_pow launches from the resident-workgroup count (beta
-    head in launch 1; every contest-a job and the contest-b jobs whose betas all ran in launch 1
-    in launch 2; the other contest-b jobs, at most one round, in launch 3; eg_capi_ballot.inc).
-    Verdicts and tally must not depend on where the splits fall: EG_POW_SLOTS forces other
-    split points (0 = no split), against the CPython tally and a tamper in the moved jobs."""
+    head in launch 1, every contest-a job in launch 2, contest b in launch 3; with
+    EG_CB_EARLY=1 launch 1 takes more betas and launch 2 the contest-b jobs they complete,
+    launch 3 keeps EG_L3_WAVES waves per SIMD of them; eg_capi_ballot.inc).  Verdicts and tally
+    must not depend on where the splits fall: EG_POW_SLOTS forces other split points (0 = no
+    split), against the CPython tally and a tamper in the moved jobs."""
     from electionguard.ballot import EncryptedBallots, Manifest, Verifier
     man = Manifest(4, 5, 1)
     nb = 700  # 16,800 selection jobs = 525 workgroups: every slot count above splits differently
     key, K, qbar, eb = _encrypt(group, man, nb, 91)
     V = Verifier(group, key, qbar, man)
     monkeypatch.setenv("EG_POW_SLOTS", slots)
-    monkeypatch.setenv("EG_L3_WAVES", l3w)  # launch 3's size in waves per SIMD
+    monkeypatch.setenv("EG_CB_EARLY", cbe)
+    monkeypatch.setenv("EG_L3_WAVES", l3w)  # launch 3's size in waves per SIMD (EG_CB_EARLY=1)
     ok_s, ok_c, tally = V.verify(eb)
     assert ok_s.all() and ok_c.all()
     assert np.array_equal(tally, _tally_products(man, eb))
