@@ -122,14 +122,16 @@ def main():
     cn = random_scalars(rng, (nb, man.n_contests), group.q)
     eb = batch_encryption(group, key, qbar, man, votes, sn, cn)  # the ballots the step verifies
     torch.cuda.synchronize()
+    # The encryption rates are N = 1 figures: at N > 1 a rank's share of configs[2] is up to
+    # 500k ballots (12 GB of ciphertexts; 61 GB with --manifest large), and a second timed
+    # encryption would hold a second copy on the host and the device.
     enc_s = None
-    # host-pointer encryption rate: best of two warm calls (same nonces, same bytes); one call at
-    # N > 1, where a rank's share of configs[2] (up to 500k ballots) makes each call seconds long
-    for _ in range(2 if world == 1 else 1):
-        t = time.perf_counter()
-        batch_encryption(group, key, qbar, man, votes, sn, cn)
-        dt = time.perf_counter() - t
-        enc_s = dt if enc_s is None else min(enc_s, dt)
+    if world == 1:
+        for _ in range(2):  # host-pointer encryption rate: best of two warm calls (same nonces, same bytes)
+            t = time.perf_counter()
+            batch_encryption(group, key, qbar, man, votes, sn, cn)
+            dt = time.perf_counter() - t
+            enc_s = dt if enc_s is None else min(enc_s, dt)
 
     dev = torch.device("cuda", local)
     d_cts = torch.from_numpy(eb.cts).to(dev)
@@ -139,15 +141,18 @@ def main():
     d_okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
     d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    enc_dev = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev,
-                                  reps=5 if world == 1 else 1)
-    enc_dev_ct = None
-    if a.ct_encrypt and world == 1:  # constant-time mode (masked table scans, no secret-indexed address): same bytes
-        group.ct_encrypt = True
-        try:
-            enc_dev_ct = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2)
-        finally:
-            group.ct_encrypt = False
+    enc_dev = enc_dev_ct = None
+    if world == 1:
+        enc_dev = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev)
+        if a.ct_encrypt:  # constant-time mode (masked table scans, no secret-indexed address): same bytes
+            group.ct_encrypt = True
+            try:
+                enc_dev_ct = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2)
+            finally:
+                group.ct_encrypt = False
+    else:
+        del eb, sn, cn  # the ranks keep only the device copy (no CPU baseline at N > 1)
+        eb = None
     # modexp/sec/GPU microbenchmark, run before the verify step so the verify
     # launches stay the last k_pow dispatches of the process (tools/prof_summary.py)
     modexp = modexp_ubench(group, a.modexp_n, dev, rank) if a.modexp_n > 0 else None
@@ -252,7 +257,7 @@ def main():
         # exponentiations (4 variable-base + 5 fixed-base per selection, 2 + 3 per contest; comb-
         # shared pairs and fused fixed-base terms counted as whole exponentiations)
         "modexp_equivalents_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
-        "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2),
+        "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2) if enc_s else None,
         "encrypt_ballots_per_s_per_gpu_device_resident": enc_dev,
         "encrypt_ballots_per_s_per_gpu_device_resident_constant_time": enc_dev_ct,
         "modexp_ubench": modexp,
