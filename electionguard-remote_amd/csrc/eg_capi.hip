@@ -180,6 +180,7 @@ struct eg_ctx {
   eg_fixed_base *g_ct = nullptr, *K_ct = nullptr;  // their kCtEncWindow-bit tables of g and K
   uint8_t K_ct_be[512];
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
+  uint32_t sel_rows = 4;                // verifier selection jobs' comb: 4 = 4 rows x 3 blocks, 0 = 5 rows x 2 blocks (EG_SEL_COMB=52)
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
   // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
   size_t pow_slots = 0;
@@ -261,9 +262,9 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
     else if (k != OP_END && k <= kOpMulLast) n.mul += 1;
   };
   const bool comb = S.comb != 0;
-  const uint32_t nb = (comb && S.blocks == 2) ? 2u : 1u;  // Lim-Lee column blocks
+  const uint32_t nb = comb ? comb_blocks(S.blocks) : 1u;  // Lim-Lee column blocks
   const uint32_t ch = comb_rows(S.rows), cw = comb_width(S.rows);  // rows, row width (bits)
-  const uint32_t bw = cw / nb;                           // columns per block
+  const uint32_t bw = comb ? comb_block_width(S.rows, S.blocks) : cw;  // columns per block (last may be shorter)
   if (S.has_base && !(comb && S.shared_comb)) {
     op(OP_LOAD_ONE);
     for (uint32_t t = 0; t < nb; ++t) op(OP_STORE_TBL, t << ch);
@@ -296,15 +297,20 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
             cslot[k] = nx++;
           }
         }
+        // comb bases B^(2^(cw r + bw t)) -> slot t * 2^h + 2^r (the chain position of each)
+        std::vector<uint32_t> bslot(257, 0);
+        for (uint32_t r = 0; r < ch; ++r)
+          for (uint32_t t = 0; t < nb; ++t) {
+            const uint32_t pos = cw * r + bw * t;
+            if (pos > 0 && pos <= 256) bslot[pos] = (t << ch) | (1u << r);
+          }
         const uint32_t kend = S.resid ? 256u : (ch - 1) * cw + (nb - 1) * bw;
         for (uint32_t k = 1; k <= kend; ++k) {
           op(OP_SQR);
-          if (k % bw == 0 && k / bw < ch * nb) {  // comb base B^(2^(cw r + bw t))
-            const uint32_t m = k / bw;
-            op(OP_STORE_TBL, ((m % nb) << ch) | (1u << (m / nb)));
-          }
-          // gather powers y_r = B^(2^(52r)) for the contest jobs (5-row combs)
-          if (ch == (uint32_t)kCombH && k % kCombW == 0 && k / kCombW < (uint32_t)kCombH)
+          if (bslot[k]) op(OP_STORE_TBL, bslot[k]);
+          // gather powers y_r = B^(2^(52r)) for the contest jobs (their 5-row combs): kept by
+          // the 5-row combs and by the verifier's selection jobs (resid) whatever their rows
+          if ((ch == (uint32_t)kCombH || S.resid) && k % kCombW == 0 && k / kCombW < (uint32_t)kCombH)
             op(OP_STORE_Y, k / kCombW - 1);
           if (k < 256 && cslot[k]) op(OP_STORE_TBL, cslot[k]);
         }
@@ -344,12 +350,14 @@ static std::vector<uint32_t> pow_schedule(const MontConsts& H, const PowShape& S
     bool one = true;
     if (S.has_base) {
       op(OP_EXP, o);
-      if (comb) {  // column w of block t is digit t * bw + w (OP_EXP)
+      if (comb) {  // column w of block t is digit t * bw + w (OP_EXP); a short last block skips its missing columns
         op(OP_LOAD_COMB, bw - 1);
-        for (uint32_t t = 1; t < nb; ++t) op(OP_MUL_COMB, t * bw + bw - 1);
+        for (uint32_t t = 1; t < nb; ++t)
+          if (t * bw + bw - 1 < cw) op(OP_MUL_COMB, t * bw + bw - 1);
         for (int w = (int)bw - 2; w >= 0; --w) {
           op(OP_SQR);
-          for (uint32_t t = 0; t < nb; ++t) op(OP_MUL_COMB, t * bw + (uint32_t)w);
+          for (uint32_t t = 0; t < nb; ++t)
+            if (t * bw + (uint32_t)w < cw) op(OP_MUL_COMB, t * bw + (uint32_t)w);
         }
       } else {
         op(OP_LOAD_WIN, o);
@@ -425,7 +433,7 @@ struct PowTail {
   const uint32_t* ctab;  // shared comb table (tail->S.shared_comb)
 };
 static size_t pow_scratch_per_group(const PowShape& S) {
-  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? ((S.blocks == 2 ? 2u : 1u) << comb_rows(S.rows)) : 16u) * kW * 4 : 4;
+  return (S.has_base && !S.shared_comb) ? (size_t)(S.comb ? (comb_blocks(S.blocks) << comb_rows(S.rows)) : 16u) * kW * 4 : 4;
 }
 // ct = true: the constant-time instantiation k_pow<F, true> for secret exponents (comb shapes
 // without fixed-base terms only); ctab: the shared comb table of S.shared_comb jobs.
@@ -449,20 +457,20 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
     return f0.wbits <= kCtMaxWindow && f1.wbits <= kCtMaxWindow;
   };
   // every population of the launch: its shape and the buffers it needs
-  auto check = [&](const PowShape& X, bool is_tail, const uint32_t* yg, const uint32_t* ro, const uint32_t* ct_tab) {
+  auto check = [&](const PowShape& X, const uint32_t* yg, const uint32_t* ro, const uint32_t* ct_tab) {
     if (X.resid && (!X.comb || X.gather || !ro)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
-    if (X.blocks > 1 && (X.blocks != 2 || !X.comb || X.gather || X.shared_comb))
-      return fail(EG_ERR_ARG, "two column blocks need a plain comb shape");
+    if (X.blocks > 1 && (X.blocks > 3 || !X.comb || X.gather || X.shared_comb))
+      return fail(EG_ERR_ARG, "two or three column blocks need a plain comb shape");
     if (X.shared_comb && (!X.comb || X.gather || X.resid || !ct_tab)) return fail(EG_ERR_ARG, "shared comb table missing");
-    if ((X.rows && is_tail) || (X.rows && (X.rows != 4 || !X.comb || X.gather || X.shared_comb || X.resid)))
-      return fail(EG_ERR_ARG, "4-row combs are plain comb shapes without residue pairs");
+    if (X.rows && (X.rows != 4 || !X.comb || X.gather || X.shared_comb))
+      return fail(EG_ERR_ARG, "4-row combs are plain comb shapes");
     if (ct && !ct_shape(X)) return fail(EG_ERR_ARG, "constant-time jobs are plain combs or small-window fixed-base terms");
     if (X.gather && (!X.comb || !yg)) return fail(EG_ERR_ARG, "gather launch needs a comb shape and y_k source");
     return (int)EG_OK;
   };
-  int src = check(S, false, ygat, rout, ctab);
-  if (!src && tail) src = check(tail->S, true, tail->ygat, tail->rout, tail->ctab);
-  if (!src && tail2) src = check(tail2->S, true, tail2->ygat, tail2->rout, tail2->ctab);
+  int src = check(S, ygat, rout, ctab);
+  if (!src && tail) src = check(tail->S, tail->ygat, tail->rout, tail->ctab);
+  if (!src && tail2) src = check(tail2->S, tail2->ygat, tail2->rout, tail2->ctab);
   if (src) return src;
   if (!njobs && !tail) return EG_OK;
   const size_t per = pow_scratch_per_group(S);
@@ -687,6 +695,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   }
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
   if (const char* cr = getenv("EG_CT_ROWS")) c->ct_rows = (cr[0] == '5') ? 0u : 4u;
+  if (const char* sc = getenv("EG_SEL_COMB")) c->sel_rows = (sc[0] == '5') ? 0u : 4u;
   if (const char* cw = getenv("EG_CT_WINDOW")) c->ct_window = std::max(4, std::min((int)kCtMaxWindow, atoi(cw)));
   {
     int cus = 0, per_cu = 0;

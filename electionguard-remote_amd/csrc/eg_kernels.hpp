@@ -395,12 +395,14 @@ struct PowShape {
                        // rout[2 gid], rout[2 gid + 1]; B^q == 1 iff z == w and B != 0 (k_resid_check)
   uint32_t shared_comb;  // comb jobs whose 32-entry subset table is PowPart::ctab (one table for every
                          // job, e.g. the trustee's g^u): no per-job precompute
-  uint32_t blocks;     // Lim-Lee column blocks v of a plain comb (0/1: one block of 52 columns, one
-                       // 32-entry table; 2: two blocks of 26, tables of B^(2^(52r)) and B^(2^(52r+26)),
-                       // 64 entries).  v = 2 pays when the squaring chain runs to 2^256 anyway (resid)
+  uint32_t blocks;     // Lim-Lee column blocks v of a plain comb (0/1: one block of cw columns, one
+                       // 2^h-entry table; 2 or 3: blocks of ceil(cw / v) columns, tables of
+                       // B^(2^(cw r + bw t)), v * 2^h entries).  v > 1 pays when the squaring chain
+                       // runs to 2^256 anyway (resid)
   uint32_t rows;       // Lim-Lee rows h of a plain comb (0: kCombH = 5 rows of 52 bits, 32-entry
                        // tables; 4: rows of 64 bits, 16-entry tables -- the constant-time trustee
-                       // pair, whose masked scans read every entry of a table)
+                       // pair, whose masked scans read every entry of a table, and the EG_SEL_COMB=43
+                       // selection jobs, 4 rows x 3 blocks)
   uint32_t fb_small[2][2];  // fixed-base term [o][t] whose scalar is < 2^wbits (the vote m of
                             // beta = K^R g^m): only radix window 0 is applied (host schedule only)
 };
@@ -441,6 +443,12 @@ constexpr int kCombH = 5;
 constexpr int kCombW = 52;
 __host__ __device__ constexpr uint32_t comb_rows(uint32_t rows) { return rows ? rows : (uint32_t)kCombH; }
 __host__ __device__ constexpr uint32_t comb_width(uint32_t rows) { return (256u + comb_rows(rows) - 1u) / comb_rows(rows); }
+// Lim-Lee column blocks v (PowShape::blocks: 0 or 1 = one table, 2 or 3 tables of 2^h entries)
+// and the columns per block, ceil(cw / v) (the last block may be shorter)
+__host__ __device__ constexpr uint32_t comb_blocks(uint32_t blocks) { return blocks > 1 ? blocks : 1u; }
+__host__ __device__ constexpr uint32_t comb_block_width(uint32_t rows, uint32_t blocks) {
+  return (comb_width(rows) + comb_blocks(blocks) - 1u) / comb_blocks(blocks);
+}
 
 __device__ __forceinline__ uint32_t be_digit(const uint8_t* __restrict__ e, int nbytes, int bit, int wb) {
   uint32_t v = 0;
@@ -543,7 +551,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
   M.load(C);
   uint32_t x[kL];
   const uint32_t ch = comb_rows(S.rows);  // comb rows: table entries per column block = 2^ch
-  const uint32_t tsize = S.comb ? ((S.blocks == 2 ? 2u : 1u) << ch) : 16u;
+  const uint32_t tsize = S.comb ? (comb_blocks(S.blocks) << ch) : 16u;
   const uint32_t gid = gid0 + threadIdx.x / kT;
   const bool live = gid < njobs;  // tail groups recompute job njobs-1 and store nothing
   const uint32_t* J = P.jobs + (size_t)(live ? gid : njobs - 1) * kJobWords;
@@ -605,14 +613,15 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
             break;
           case OP_EXP:
             if (S.comb) {
-              // column digits of exponent J[1 + arg]: bit j of each of the 5 rows (52 bits each); with
-              // two column blocks, columns 26..51 index the second table (entry 32 + digit)
+              // column digits of exponent J[1 + arg]: bit j of each of the h rows (cw bits each);
+              // with v column blocks of bw = ceil(cw / v) columns, column j indexes table j / bw
+              // (entry (j / bw) * 2^h + digit)
               const uint8_t* e = scalars + (size_t)J[1 + arg] * 32;
               const int cw = (int)comb_width(S.rows);
-              const int hi = S.blocks == 2 ? cw / 2 : cw;
+              const int bw = (int)comb_block_width(S.rows, S.blocks);
               wave_sync();
               for (int j = glane(); j < cw; j += kT) {
-                uint32_t d = j >= hi ? (1u << ch) : 0u;
+                uint32_t d = (uint32_t)(j / bw) << ch;
 #pragma unroll
                 for (int r = 0; r < kCombH; ++r) {
                   const int bit = r * cw + j;

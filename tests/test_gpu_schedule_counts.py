@@ -1,11 +1,13 @@
 """GPU: the Montgomery-multiply counts of the op programs k_pow runs, pinned per unit of
 work (eg_ctx_profile_end counts them from the programs of the timed launches):
 
-* verifier, 4 x (5+1) manifest: per selection the alpha job's 465 + 2 W and the beta job's
-  465 + 3 W (256-step squaring chain, 5 for w = B^189, 2 x 26 two-block subset products,
-  2 x 76 comb, then 2 or 3 fixed-base terms of W = ceil(256 / window bits) table windows
-  each), per contest 148 + W (A) and 148 + 2 W (B) gathered combs: 25,088 MM per ballot at
-  the bench's 22-bit tables (W = 12), 27,728 at the default 8-bit ones (W = 32);
+* verifier, 4 x (5+1) manifest: per selection the alpha job's 462 + 2 W and the beta job's
+  462 + 3 W (256-step squaring chain, 5 for w = B^189, 3 x 11 subset products of the 4-row,
+  3-block comb, 2 x (21 + 63) comb evaluation, then 2 or 3 fixed-base terms of
+  W = ceil(256 / window bits) table windows each), per contest 148 + W (A) and 148 + 2 W (B)
+  gathered combs: 24,944 MM per ballot at the bench's 22-bit tables (W = 12), 27,584 at the
+  default 8-bit ones (W = 32) (round 2's 5-row, 2-block comb, EG_SEL_COMB=52: 465 + ... and
+  25,088);
 * trustee share: 434 MM for the constant-time 4-row comb pair (A^s, A^u) + 102 for g^u
   from g's shared comb table.
 The verdicts of the profiled batches are checked too (the counts are of real work)."""
@@ -18,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 def verify_mm_per_ballot(window_bits: int) -> int:
     W = -(-256 // window_bits)
-    return 24 * ((465 + 2 * W) + (465 + 3 * W)) + 4 * ((148 + W) + (148 + 2 * W))
+    return 24 * ((462 + 2 * W) + (462 + 3 * W)) + 4 * ((148 + W) + (148 + 2 * W))
 
 
 TRUSTEE_MM_PER_TEXT = (224 + 2 * 11 + 2 * (31 + 63)) + (1 + 51 * 2 - 1)
@@ -27,7 +29,7 @@ TRUSTEE_MM_PER_TEXT = (224 + 2 * 11 + 2 * (31 + 63)) + (1 + 51 * 2 - 1)
 def test_verifier_mm_per_ballot(group):
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption, random_scalars, random_votes
     from electionguard.keyceremony import key_ceremony
-    assert verify_mm_per_ballot(22) == 25088 and verify_mm_per_ballot(8) == 27728
+    assert verify_mm_per_ballot(22) == 24944 and verify_mm_per_ballot(8) == 27584
     man = Manifest(4, 5, 1)
     _, K = key_ceremony(group, 3, 3, seed=5)
     key = ElectionKey(group, K)

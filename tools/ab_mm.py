@@ -130,6 +130,8 @@ if __name__ == "__main__":
             env_extra["EG_CB_EARLY"] = "0"
         if "@cbe" in name:  # early contest-b jobs in launch 2 (opt-in schedule)
             env_extra["EG_CB_EARLY"] = "1"
+        if "@sel43" in name:  # verifier selection jobs on the 4-row, 3-block comb
+            env_extra["EG_SEL_COMB"] = "43"
         if "@l3w" in name:  # with @cbe: launch 3 sized to 1..3 waves per SIMD (default 2)
             env_extra["EG_CB_EARLY"] = "1"
             env_extra["EG_L3_WAVES"] = name.split("@l3w")[1][:1]
