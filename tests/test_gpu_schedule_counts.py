@@ -46,6 +46,44 @@ def test_verifier_mm_per_ballot(group):
     assert kp.mont_ops == nb * verify_mm_per_ballot(key.window_bits), kp
 
 
+def test_verifier_comb52_same_verdicts_and_tally(group, monkeypatch):
+    """EG_SEL_COMB=52 (read at context creation) puts the selection jobs back on round 2's
+    5-row, 2-block comb: its op programs cost 465 + 2 W / 465 + 3 W per alpha / beta job (25,088
+    MM per ballot at W = 12), and its verdicts and tally equal the default 4 x 3 comb's, on
+    honest ballots and with one tampered proof."""
+    from electionguard.ballot import (ElectionKey, EncryptedBallots, Manifest, Verifier, batch_encryption,
+                                      random_scalars, random_votes)
+    from electionguard.core import GroupContext
+    from electionguard.keyceremony import key_ceremony
+    monkeypatch.setenv("EG_SEL_COMB", "52")
+    g52 = GroupContext(group.p, group.q, group.g, device=group.device)
+    man = Manifest(4, 5, 1)
+    _, K = key_ceremony(group, 3, 3, seed=6)
+    rng = np.random.default_rng(10)
+    nb = 200
+    eb = batch_encryption(group, ElectionKey(group, K), 77, man, random_votes(rng, man, nb),
+                          random_scalars(rng, (nb, man.nsel, 4), group.q), random_scalars(rng, (nb, man.n_contests), group.q))
+    rp = eb.rproof.copy()
+    rp[17, 5, 1, 3] ^= 0x40
+    bad = EncryptedBallots(eb.cts, rp, eb.cproof)
+    W = -(-256 // 8)
+    for G in (group, g52):
+        V = Verifier(G, ElectionKey(G, K), 77, man)
+        V.verify(eb.slice(0, 1))  # warm-up outside the profile window
+        G.profile_begin()
+        ok_s, ok_c, tally = V.verify(eb)
+        kp = G.profile_end()
+        assert ok_s.all() and ok_c.all()
+        per_job = (465, 465) if G is g52 else (462, 462)
+        assert kp.mont_ops == nb * (24 * ((per_job[0] + 2 * W) + (per_job[1] + 3 * W)) + 4 * ((148 + W) + (148 + 2 * W))), kp
+        ok_s2, ok_c2, _ = V.verify(bad, with_tally=False)
+        assert np.argwhere(~ok_s2).tolist() == [[17, 5]] and ok_c2.all()
+        if G is group:
+            ref_tally = tally
+        else:
+            assert np.array_equal(tally, ref_tally)
+
+
 def test_trustee_mm_per_text(group):
     from electionguard.ballot import random_scalars
     from electionguard.decrypt import partial_decrypt_batch
