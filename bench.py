@@ -5,17 +5,27 @@ selections per ballot), batch-encrypted on the GPU in setup (untimed, reported s
 then ONE step = verify every ballot's disjunctive and contest proofs + homomorphic tally of all
 ballots, with the encrypted ballots already resident in HBM.
   * N = 1: BASELINE.json configs[1], 10k ballots on one GPU.
-  * N > 1 (torch.distributed.run or self-launched, one rank per GPU): configs[2], 1M ballots
-    over the node, 1_000_000 // N contiguous ballots per rank (a fixed total: strong scaling);
-    the per-rank partial tallies are all-gathered over RCCL and folded mod p on rank 0.
+  * N > 1 (torch.distributed.run or self-launched, one rank per GPU): configs[2]'s per-GPU shard,
+    125,000 contiguous ballots per rank (weak scaling; N = 8 is configs[2] itself, 1M ballots over
+    the node); the per-rank partial tallies are all-gathered over RCCL and folded mod p on rank 0.
   * --manifest large: the configs[4] manifest (20 contests x 5 selections, 120 encrypted
     selections per ballot), same ballot counts unless --ballots is given.
+  * --pipeline full: configs[4]'s full pipeline per step (device encryption, verify + tally, the
+    all-gather fold and, on rank 0, the threshold decryption through 5 DecryptingTrustees with
+    exact counts); see full_pipeline().
+
+Every device buffer, kernel and collective runs through libeg_hip.so (its own HIP runtime and
+its own RCCL communicator, include/eg_hip.h): torch is imported only for its CPU process group
+(gloo), which carries the RCCL id, barriers and the max-over-ranks time, and never initialises
+the GPU.  The step is bracketed by a barrier + a device synchronisation of the library's stream
+(group.sync(), the eg_ctx_sync of every kernel the step queued) on both sides.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the roofline definition.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -31,100 +41,160 @@ PEAK_TMAC = 256 * 64 * 2.4e9 / 1e12   # 256 CUs x 64 v_mad_u64_u32 lanes/clk/CU 
 # measured v_mad_u64_u32 issue ceiling at 3 waves/SIMD (k_pow's occupancy): 58.4 lane-MAC/clk/CU,
 # 4.4 cycles per wave-instruction (profiles/r01_ubench_banks.txt)
 ISSUE_TMAC = 256 * 58.4 * 2.4e9 / 1e12
+SHARD = 125_000  # ballots per GPU at N > 1: configs[2]'s 1M ballots over 8 GPUs
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--ballots", type=int, default=0,
-                    help="ballots per GPU (0 = the config's: 10k at N = 1 (configs[1]), 1M // N for N > 1 (configs[2]))")
-    ap.add_argument("--manifest", choices=("small", "large"), default="small",
-                    help="small = 4 contests x 5 selections (configs[1-2]); large = 20 x 5 (configs[4])")
+                    help="ballots per GPU (0 = the config's: 10k at N = 1 (configs[1]), 125k per GPU at N > 1 "
+                         "(configs[2]'s shard) and for --pipeline full (configs[4]'s shard))")
+    ap.add_argument("--manifest", choices=("small", "large"), default=None,
+                    help="small = 4 contests x 5 selections (configs[1-2]); large = 20 x 5 (configs[4]; the "
+                         "default of --pipeline full)")
     ap.add_argument("--contests", type=int, default=0, help="override the manifest's contests")
     ap.add_argument("--selections", type=int, default=5)
+    ap.add_argument("--pipeline", choices=("verify", "full"), default="verify",
+                    help="verify = verify + tally (the metric); full = encrypt + verify + tally + fold + "
+                         "threshold decryption per step (configs[4])")
+    ap.add_argument("--guardians", type=int, default=5, help="--pipeline full: guardians (configs[3-4]: 5)")
+    ap.add_argument("--quorum", type=int, default=3)
+    ap.add_argument("--available", type=int, default=3, help="--pipeline full: guardians present at decryption")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds a collective (and the rank launcher) may wait before failing")
     ap.add_argument("--fb-window", type=int, default=22, help="fixed-base radix window bits for g and K")
     ap.add_argument("--cpu-sample", type=int, default=1, help="run the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the affinity count)")
+    ap.add_argument("--cpu-max-ballots", type=int, default=2000,
+                    help="ballots rank 0 keeps on the host for the CPU baseline at N > 1")
     ap.add_argument("--modexp-n", type=int, default=1 << 20,
-                    help="modexp microbenchmark batch per GPU (SURVEY 8(d): 2^20; 0 = skip)")
+                    help="modexp microbenchmark batch (SURVEY 8(d): 2^20; rank 0 only; 0 = skip)")
     ap.add_argument("--ct-encrypt", type=int, default=1,
                     help="also time the constant-time encryption mode (eg_ctx_set_ct_encrypt; 0 = skip)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.manifest is None:
+        a.manifest = "large" if a.pipeline == "full" else "small"
     if not a.contests:
         a.contests = 20 if a.manifest == "large" else 4
     if not a.ballots:
-        a.ballots = default_ballots(a.gpus)
+        a.ballots = default_ballots(a.gpus, a.pipeline)
     return a
 
 
-def default_ballots(gpus: int) -> int:
+def default_ballots(gpus: int, pipeline: str = "verify") -> int:
     """Ballots per GPU of the BASELINE config bench.py measures at N GPUs: configs[1] (10k on one
-    GPU) at N = 1, configs[2] (1M ballots over the node) at N > 1."""
-    return 10_000 if gpus <= 1 else 1_000_000 // gpus
+    GPU) at N = 1; configs[2]'s per-GPU shard (125k = 1M / 8) at N > 1, so every N runs the same
+    per-GPU work (weak scaling) and N = 8 is configs[2] exactly; --pipeline full: configs[4]'s
+    per-GPU shard (125k ballots of 20 x (5+1)) at every N."""
+    if pipeline == "full":
+        return SHARD
+    return 10_000 if gpus <= 1 else SHARD
 
 
-def main():
-    a = parse()
-    from electionguard.launch import launched_world, run_ranks
+def config_name(contests: int, selections: int, nb: int, world: int) -> str:
+    """BASELINE.json config this run measures: configs[1] = 10k ballots of 4 x 5 on ONE GPU;
+    configs[2] = 1M ballots of 4 x 5 over the node (125k per GPU at N = 8); configs[4] = 1M
+    ballots of the 100-selection manifest (20 x 5) at 1/2/4/8 GPUs."""
+    total = nb * world
+    gpus = f"{world} GPU{'s' if world > 1 else ''}"
+    if (contests, selections) == (4, 5):
+        if total == 1_000_000:
+            return f"configs[2] (1M ballots over {gpus})"
+        if world == 1 and nb == 10_000:
+            return "configs[1]"
+        if nb == SHARD:
+            return f"configs[2] per-GPU shard ({SHARD} ballots per GPU x {gpus})"
+        return f"configs[1] shape (4x5), {nb} ballots per GPU x {gpus}"
+    if (contests, selections) == (20, 5):
+        if total == 1_000_000:
+            return f"configs[4] (1M ballots of 20x5 over {gpus})"
+        if nb == SHARD:
+            return f"configs[4] per-GPU shard ({SHARD} ballots of 20x5 per GPU x {gpus})"
+        return f"configs[4] shape (20x5), {nb} ballots per GPU x {gpus}"
+    return f"custom manifest {contests}x{selections}, {nb} ballots per GPU x {gpus}"
+
+
+def exchange_mode() -> str:
+    """EG_DIST_BACKEND=gloo rehearses N > 1 with host collectives (every rank may share one GPU);
+    the default is libeg_hip's RCCL communicator ("nccl" is accepted for it)."""
+    m = os.environ.get("EG_DIST_BACKEND", "rccl").lower()
+    return "gloo" if m == "gloo" else "rccl"
+
+
+def init_ranks(a):
+    """-> (world, rank, device, dist): the host process group (gloo, CPU only) at N > 1."""
+    from electionguard.launch import launched_world
     lw = launched_world()
-    if lw is None and a.gpus > 1:
-        # no launcher: start one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*) before
-        # anything touches HIP; rank 0 prints the JSON line; the first rank to fail ends the run
-        # (the others are killed) and its status is this process's
-        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus, timeout=a.dist_timeout * 4))
     if lw is not None and lw != a.gpus:
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={lw} ranks")
     world = lw or 1
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-
+    if exchange_mode() == "gloo":
+        local = 0  # the rehearsal puts every rank on one GPU
     dist = None
-    # EG_DIST_BACKEND=gloo rehearses the N>1 path with every rank on one GPU (host collectives)
-    backend = os.environ.get("EG_DIST_BACKEND", "nccl")
-    if backend == "gloo":
-        local = 0
     if world > 1:
         import datetime
 
         import torch.distributed as dist
+        # a dead peer fails the collective instead of hanging it
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=a.dist_timeout))
+    return world, rank, local, dist
 
-        torch.cuda.set_device(local)
-        tmo = datetime.timedelta(seconds=a.dist_timeout)  # a dead peer fails the collective, not hangs it
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
-        else:
-            dist.init_process_group(backend, timeout=tmo)
+
+def main(argv=None):
+    a = parse(argv)
+    from electionguard.launch import launched_world, run_ranks
+    if launched_world() is None and a.gpus > 1:
+        # no launcher: start one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*) before
+        # anything touches HIP; rank 0 prints the JSON line; the first rank to fail ends the run
+        # (the others are killed) and its status is this process's
+        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus, timeout=a.dist_timeout * 4))
+    world, rank, local, dist = init_ranks(a)
+    if a.pipeline == "full":
+        out = full_pipeline(a, world, rank, local, dist)
     else:
-        torch.cuda.set_device(local)
+        out = verify_tally(a, world, rank, local, dist)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
-    from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption, random_scalars,
-                                      random_votes)
-    from electionguard.core import productionGroup
-    from electionguard.distributed import all_valid, gather_fold_tally
+
+def setup_election(a, group, rank):
+    """Synthetic election shared by every rank (3 guardians, quorum 3: configs[0]'s shape; or the
+    --pipeline full trustees) and this rank's ballots (votes, nonces)."""
+    from electionguard.ballot import ElectionKey, Manifest, random_scalars, random_votes
     from electionguard.keyceremony import key_ceremony
-
-    group = productionGroup(local)
     man = Manifest(a.contests, a.selections, 1)
-    nb = a.ballots
-    # synthetic election: 3 guardians, quorum 3 (configs[0] shape), same on every rank
-    gk, K = key_ceremony(group, 3, 3, seed=20241015)
+    n_g, quorum = (a.guardians, a.quorum) if a.pipeline == "full" else (3, 3)
+    gk, K = key_ceremony(group, n_g, quorum, seed=20241015)
     key = ElectionKey(group, K, window_bits=a.fb_window)
     qbar = int.from_bytes(b"electionguard-remote mi355x qbar".ljust(32, b"\0"), "big") % group.q
     rng = np.random.default_rng(1000 + rank)
+    nb = a.ballots
     votes = random_votes(rng, man, nb)
     sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
     cn = random_scalars(rng, (nb, man.n_contests), group.q)
+    return man, gk, K, key, qbar, votes, sn, cn
+
+
+def verify_tally(a, world, rank, local, dist):
+    """configs[1] / configs[2] (--manifest large: configs[4]): one step = verify + tally of the
+    rank's resident ballots, the verdict all-reduce and the tally all-gather + fold."""
+    from electionguard.ballot import Verifier, batch_encryption
+    from electionguard.core import productionGroup
+    from electionguard.distributed import TallyExchange, max_over_ranks
+
+    group = productionGroup(local)
+    man, _, K, key, qbar, votes, sn, cn = setup_election(a, group, rank)
+    nb = a.ballots
     eb = batch_encryption(group, key, qbar, man, votes, sn, cn)  # the ballots the step verifies
-    torch.cuda.synchronize()
-    # The encryption rates are N = 1 figures: at N > 1 a rank's share of configs[2] is up to
-    # 500k ballots (12 GB of ciphertexts; 61 GB with --manifest large), and a second timed
-    # encryption would hold a second copy on the host and the device.
+    # The encryption rates are N = 1 figures (at N > 1 a rank keeps only its device copy).
     enc_s = None
     if world == 1:
         for _ in range(2):  # host-pointer encryption rate: best of two warm calls (same nonces, same bytes)
@@ -132,40 +202,37 @@ def main():
             batch_encryption(group, key, qbar, man, votes, sn, cn)
             dt = time.perf_counter() - t
             enc_s = dt if enc_s is None else min(enc_s, dt)
-
-    dev = torch.device("cuda", local)
-    d_cts = torch.from_numpy(eb.cts).to(dev)
-    d_rp = torch.from_numpy(eb.rproof).to(dev)
-    d_cp = torch.from_numpy(eb.cproof).to(dev)
-    d_oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
-    d_okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
-    d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
+    d_cts, d_rp, d_cp = (group.to_device(x) for x in (eb.cts, eb.rproof, eb.cproof))
+    d_oks = group.device_buffer(nb * man.nsel)
+    d_okc = group.device_buffer(nb * man.n_contests)
+    d_tal = group.device_buffer(man.n_real * 2 * 512)
     enc_dev = enc_dev_ct = None
     if world == 1:
-        enc_dev = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev)
+        enc_dev = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp)
         if a.ct_encrypt:  # constant-time mode (masked table scans, no secret-indexed address): same bytes
             group.ct_encrypt = True
             try:
-                enc_dev_ct = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=2)
+                enc_dev_ct = encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, reps=2)
             finally:
                 group.ct_encrypt = False
-    else:
-        del eb, sn, cn  # the ranks keep only the device copy (no CPU baseline at N > 1)
-        eb = None
-    # modexp/sec/GPU microbenchmark, run before the verify step so the verify
+    # rank 0 keeps a bounded host sample of its ballots for the CPU baseline (at N = 1 the whole
+    # batch stays: the sample is sized from a calibration run); the other ranks keep none
+    sample = eb if world == 1 else (eb.slice(0, min(nb, a.cpu_max_ballots)) if rank == 0 else None)
+    if sample is not None and world > 1:
+        sample = type(eb)(sample.cts.copy(), sample.rproof.copy(), sample.cproof.copy())
+    del eb, sn, cn
+    # modexp/sec/GPU microbenchmark on rank 0, before the verify step so the verify
     # launches stay the last k_pow dispatches of the process (tools/prof_summary.py)
-    modexp = modexp_ubench(group, a.modexp_n, dev, rank) if a.modexp_n > 0 else None
+    modexp = modexp_ubench(group, a.modexp_n, rank) if a.modexp_n > 0 and rank == 0 else None
+    xch = TallyExchange(group, dist, world, rank, exchange_mode())
     ver = Verifier(group, key, qbar, man)
     final_tally = None
 
     def step():
         nonlocal final_tally
-        ver.verify_device(d_cts.data_ptr(), d_rp.data_ptr(), d_cp.data_ptr(), nb, d_oks.data_ptr(),
-                          d_okc.data_ptr(), d_tal.data_ptr())
-        group.sync()  # ctx stream -> torch stream ordering for the collective
-        ok = all_valid(dist, bool(d_oks.all().item() and d_okc.all().item()), dev)
-        final_tally = gather_fold_tally(dist, d_tal, group.prodP_groups)
+        ver.verify_device(d_cts.ptr, d_rp.ptr, d_cp.ptr, nb, d_oks.ptr, d_okc.ptr, d_tal.ptr)
+        ok = xch.all_valid(group.all_nonzero(d_oks) and group.all_nonzero(d_okc))
+        final_tally = xch.fold(d_tal, man.n_real)
         if not ok:
             raise RuntimeError("verification failed on honest synthetic ballots")
 
@@ -173,41 +240,66 @@ def main():
         step()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    group.sync()
     group.profile_begin()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     group.sync()
-    torch.cuda.synchronize()
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
     kp = group.profile_end()
-    kms, kmm, klaunch = kp.ms, kp.mont_ops, kp.launches
-    if dist:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    el = max_over_ranks(dist, el)
+    xch.close()
 
+    value = nb * world * a.steps / el
+    out = line_common(a, world, el, value, kp, nb, man, "ballots verified+tallied/sec (node, 4096-bit group)",
+                      xch.collective)
+    out["modexp_per_s_per_gpu"] = {"var_base": modexp.get("var_base_per_s"),
+                                   "fixed_base_g": modexp.get("fixed_base_g_per_s")} if modexp else None
+    # a derived count, not a measurement: the verify step's work expressed in 256-bit
+    # exponentiations (4 variable-base + 5 fixed-base per selection, 2 + 3 per contest; comb-
+    # shared pairs and fused fixed-base terms counted as whole exponentiations)
+    out["modexp_equivalents_per_s_per_gpu"] = round((9 * man.nsel + 5 * man.n_contests) * value / world, 1)
+    out["encrypt_ballots_per_s_per_gpu"] = round(nb / enc_s, 2) if enc_s else None
+    out["encrypt_ballots_per_s_per_gpu_device_resident"] = enc_dev
+    out["encrypt_ballots_per_s_per_gpu_device_resident_constant_time"] = enc_dev_ct
+    out["modexp_ubench"] = modexp
+    return report(a, out, world, rank, dist, man, sample, qbar, K)
+
+
+def report(a, out, world, rank, dist, man, sample, qbar, K):
+    """After the timed steps: every rank meets at a barrier, then rank 0 alone times the CPU port
+    on its host sample (the other ranks are done, so it has the host's cores) and the line gets
+    cpu_baseline and vs_baseline at every N."""
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and a.cpu_sample > 0 and sample is not None:
+        out["cpu_baseline"] = cpu_baseline(a, man, sample, qbar, K)
+        attach_ratio(out)
+    return out
+
+
+def line_common(a, world, el, value, kp, nb, man, metric, collective):
+    """The bench line's fields every mode shares (value, roofline of k_pow, config)."""
     from electionguard.core import native
     radix = native.version().split("radix2^")[1].split()[0]
-    import hashlib
     build_id = hashlib.md5(Path(native.lib_path()).read_bytes()).hexdigest()[:12]
-    total_ballots = nb * world * a.steps
     cfg_name = config_name(a.contests, a.selections, nb, world)
+    kms, kmm, klaunch = kp.ms, kp.mont_ops, kp.launches
     clock = kp.clock_ghz if kp.clock_ghz and 1.0 <= kp.clock_ghz <= 2.6 else None
     clock_note = (f"median of {kp.clock_records} workgroup records, {kp.clock_dropped} dropped" if clock else
                   f"null: median {kp.clock_ghz:.3f} GHz outside [1.0, 2.6] ({kp.clock_records} records used, "
                   f"{kp.clock_dropped} dropped as unset, wrapped or out of range)")
-    coll = "RCCL" if (dist is None or backend == "nccl") else backend
-    value = total_ballots / el
     # algorithmic work of the dominant kernel (k_pow), from its own launch schedule:
     # 2*128^2 u32 MACs per multiply, 128*129/2 + 128^2 per squaring (group.MAC_PER_*)
     achieved = kp.macs / (kms / 1e3) / 1e12 if kms > 0 else None
     mm_per_ballot = kmm / (nb * a.steps) if a.steps else None
+    what = ("encrypt + verify + tally + fold + threshold decryption" if a.pipeline == "full"
+            else "verify + homomorphic tally")
     out = {
-        "metric": "ballots verified+tallied/sec (node, 4096-bit group)",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "ballots/s",
         "n_gpus": world,
@@ -215,18 +307,17 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(el / a.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong" if world > 1 and nb * world == 1_000_000 else "weak",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": f"u32xu32->u64 (radix-2^{radix} limbs)",
         "data": "synthetic (seeded random one-hot ballots, GPU-encrypted with random nonces)",
         "config": {
-            "workload": f"{cfg_name}: verify + homomorphic tally of {nb} ballots per GPU "
-                        f"({nb * world} in total), {a.contests} contests x {a.selections} selections "
-                        "(+1 placeholder), EG 1.0 4096-bit production group",
+            "workload": f"{cfg_name}: {what} of {nb} ballots per GPU ({nb * world} in total), {a.contests} contests "
+                        f"x {a.selections} selections (+1 placeholder), EG 1.0 4096-bit production group",
             "ballots_per_gpu": nb,
             "selections_per_ballot": man.nsel,
             "fb_window_bits": a.fb_window,
-            "parallelism": f"ballot-sharded x{world}, {coll} all-gather of partial tallies",
+            "parallelism": f"ballot-sharded x{world}, {collective} all-gather of partial tallies",
         },
         "roofline": {
             "bound": "valu-int",
@@ -249,20 +340,10 @@ def main():
             "squaring_frac": round(kp.squarings / kmm, 4) if kmm else None,
         },
         "mont_ops_per_ballot": round(mm_per_ballot, 1) if mm_per_ballot else None,
-        # BASELINE's second metric, MEASURED by the modexp microbenchmark (2^20 independent
-        # 256-bit exponentiations per GPU, operands in HBM): variable base and fixed base g
-        "modexp_per_s_per_gpu": {"var_base": modexp.get("var_base_per_s"), "fixed_base_g": modexp.get("fixed_base_g_per_s")}
-        if modexp else None,
-        # a derived count, not a measurement: the verify step's work expressed in 256-bit
-        # exponentiations (4 variable-base + 5 fixed-base per selection, 2 + 3 per contest; comb-
-        # shared pairs and fused fixed-base terms counted as whole exponentiations)
-        "modexp_equivalents_per_s_per_gpu": round((9 * man.nsel + 5 * man.n_contests) * value / world, 1),
-        "encrypt_ballots_per_s_per_gpu": round(nb / enc_s, 2) if enc_s else None,
-        "encrypt_ballots_per_s_per_gpu_device_resident": enc_dev,
-        "encrypt_ballots_per_s_per_gpu_device_resident_constant_time": enc_dev_ct,
-        "modexp_ubench": modexp,
         "build": build_id,
     }
+    if a.pipeline == "full":
+        out["config"]["pipeline"] = "full"
     # HBM traffic of k_pow from the committed PMC passes of this same command
     # (tools/profile_round.sh); only quoted when the profiled workload AND the library build
     # (md5 of libeg_hip.so) match this run's.
@@ -275,50 +356,32 @@ def main():
                 break
         except (KeyError, ValueError, TypeError):
             pass
-
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(a, man, eb, qbar, K, final_tally)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return out
 
 
-def config_name(contests: int, selections: int, nb: int, world: int) -> str:
-    """BASELINE.json config this run measures: configs[1] = 10k ballots of 4 x 5 on ONE GPU;
-    configs[2] = 1M ballots of 4 x 5 over the node; configs[4] = 1M ballots of the 100-selection
-    manifest (20 x 5) at 1/2/4/8 GPUs."""
-    total = nb * world
-    gpus = f"{world} GPU{'s' if world > 1 else ''}"
-    if (contests, selections) == (4, 5):
-        if total == 1_000_000:
-            return f"configs[2] (1M ballots over {gpus})"
-        if world == 1 and nb == 10_000:
-            return "configs[1]"
-        return f"configs[1] shape (4x5), {nb} ballots per GPU x {gpus}"
-    if (contests, selections) == (20, 5):
-        if total == 1_000_000:
-            return f"configs[4] (1M ballots of 20x5 over {gpus})"
-        return f"configs[4] shape (20x5), {nb} ballots per GPU x {gpus}"
-    return f"custom manifest {contests}x{selections}, {nb} ballots per GPU x {gpus}"
+def attach_ratio(out):
+    """vs_baseline = value / cpu_baseline.value: BASELINE.json publishes no number for this metric,
+    and the north_star's target (>= 50x on 8 GPUs) is defined against the host-CPU path timed on the
+    box's cores in the same run, which cpu_baseline is (same workload shape, cores stated)."""
+    cb = out.get("cpu_baseline")
+    if cb and cb.get("value"):
+        out["vs_baseline"] = round(out["value"] / cb["value"], 2)
+        out["vs_baseline_basis"] = (f"value / cpu_baseline.value: the CPU port of the same step on {cb['cores']} "
+                                    f"host cores in this run (BASELINE.json publishes no number)")
 
 
-def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, dev, reps=5):
+def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp, reps=5):
     """batch-encrypt with votes, nonces and outputs resident in HBM (eg_encrypt_ballots_dev),
     best of `reps` timed runs; the outputs must equal the host-pointer encryption's bytes
     (same injected nonces) already resident in d_cts / d_rp / d_cp."""
-    import torch
-
     from electionguard.ballot import batch_encryption_device
 
     nb = votes.shape[0]
-    dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (votes, sn, cn))
-    oc, orp, ocp = torch.empty_like(d_cts), torch.empty_like(d_rp), torch.empty_like(d_cp)
-    torch.cuda.synchronize()
+    dv, dsn, dcn = (group.to_device(x) for x in (votes, sn, cn))
+    oc, orp, ocp = (group.device_buffer(x.nbytes) for x in (d_cts, d_rp, d_cp))
 
     def run():
-        batch_encryption_device(group, key, qbar, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
-                                oc.data_ptr(), orp.data_ptr(), ocp.data_ptr())
+        batch_encryption_device(group, key, qbar, man, nb, dv.ptr, dsn.ptr, dcn.ptr, oc.ptr, orp.ptr, ocp.ptr)
 
     run()
     best = None
@@ -327,36 +390,34 @@ def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp,
         run()
         dt = time.perf_counter() - t
         best = dt if best is None else min(best, dt)
-    if not (torch.equal(oc, d_cts) and torch.equal(orp, d_rp) and torch.equal(ocp, d_cp)):
+    same = all(np.array_equal(x.download(), y.download()) for x, y in ((oc, d_cts), (orp, d_rp), (ocp, d_cp)))
+    for b in (dv, dsn, dcn, oc, orp, ocp):
+        b.free()
+    if not same:
         raise RuntimeError("device-resident encryption differs from the host-pointer encryption")
-    del dv, dsn, dcn, oc, orp, ocp
-    torch.cuda.empty_cache()
     return round(nb / best, 2)
 
 
-def modexp_ubench(group, n, dev, rank, reps=2):
+def modexp_ubench(group, n, rank, reps=2):
     """SURVEY 8(d) modexp microbenchmark on one GPU: n variable-base powP (bases g^x, x and the
     exponents uniform in [1, q)) and n fixed-base gPowP, operands resident in HBM
     (eg_powp_batch_dev / eg_fb_pow_batch_dev); a few results are spot-checked with CPython pow."""
-    import torch
-
     rng = np.random.default_rng(7 + rank)
     q, p, g = group.q, group.p, group.g
 
     def scalars(m):  # uniform 256-bit: in [1, q) except with probability 2^-248 (used as given)
         return rng.integers(0, 256, size=(m, 32), dtype=np.uint8)
 
-    xs = torch.from_numpy(scalars(n)).to(dev)
-    es = torch.from_numpy(scalars(n)).to(dev)
-    bases = torch.empty((n, 512), dtype=torch.uint8, device=dev)
-    out = torch.empty((n, 512), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
-    group.gPowP_batch_dev(xs.data_ptr(), bases.data_ptr(), n)  # bases g^x (subgroup elements)
-    group.powP_batch_dev(bases.data_ptr(), es.data_ptr(), out.data_ptr(), n)  # warm-up (job table)
+    xs_h, es_h = scalars(n), scalars(n)
+    xs, es = group.to_device(xs_h), group.to_device(es_h)
+    bases = group.device_buffer(n * 512)
+    out = group.device_buffer(n * 512)
+    group.gPowP_batch_dev(xs.ptr, bases.ptr, n)  # bases g^x (subgroup elements)
+    group.powP_batch_dev(bases.ptr, es.ptr, out.ptr, n)  # warm-up (job table)
     group.sync()
     res = {"n": n, "exponent_bits": 256, "reps": reps}
-    for name, run in (("var_base", lambda: group.powP_batch_dev(bases.data_ptr(), es.data_ptr(), out.data_ptr(), n)),
-                      ("fixed_base_g", lambda: group.gPowP_batch_dev(es.data_ptr(), out.data_ptr(), n))):
+    for name, run in (("var_base", lambda: group.powP_batch_dev(bases.ptr, es.ptr, out.ptr, n)),
+                      ("fixed_base_g", lambda: group.gPowP_batch_dev(es.ptr, out.ptr, n))):
         run()
         group.sync()
         group.profile_begin()
@@ -370,26 +431,22 @@ def modexp_ubench(group, n, dev, rank, reps=2):
         res[f"{name}_mont_ops_per_exp"] = round(kp.mont_ops / (n * reps), 1)
         res[f"{name}_kpow_tmac_s"] = round(kp.macs / (kp.ms / 1e3) / 1e12, 3) if kp.ms > 0 else None
         # spot check the last run's first and last results (CPython pow; not the oracle)
-        ob, xb, eb_ = out.cpu().numpy(), xs.cpu().numpy(), es.cpu().numpy()
+        ob = out.download().reshape(n, 512)
         for i in (0, n - 1):
-            e = int.from_bytes(eb_[i].tobytes(), "big")
-            b = pow(g, int.from_bytes(xb[i].tobytes(), "big"), p) if name == "var_base" else g
+            e = int.from_bytes(es_h[i].tobytes(), "big")
+            b = pow(g, int.from_bytes(xs_h[i].tobytes(), "big"), p) if name == "var_base" else g
             if int.from_bytes(ob[i].tobytes(), "big") != pow(b, e, p):
                 raise RuntimeError(f"modexp microbenchmark {name}: result {i} differs from pow()")
     res["spot_checked"] = True
-    del xs, es, bases, out
-    torch.cuda.empty_cache()
+    for b in (xs, es, bases, out):
+        b.free()
     return res
 
 
-def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
-    """C restatement of the JVM path (OpenSSL BN Montgomery sliding window, 8-bit radix
-    fixed base = LOW_MEMORY_USE) on a bounded sample of the same ballots, on every host core
-    this process may run on (sched_getaffinity), sized to about --cpu-seconds of work."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    from eg_oracle_c import COracle
-    from electionguard.core import constants as C
-
+def cpu_threads(a):
+    """Threads of the CPU baseline: every core the lease lets this process use -- the affinity set,
+    capped by the cgroup CPU quota (more threads than the quota only time-slice: 256 threads under
+    a 16-CPU quota ran 38% slower)."""
     affinity = len(os.sched_getaffinity(0))
     quota_cpus = None
     try:  # a cgroup CPU quota caps the useful parallelism below the affinity count
@@ -398,9 +455,30 @@ def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
             quota_cpus = int(q[0]) / int(q[1])
     except (OSError, ValueError, IndexError):
         pass
-    # every core the lease lets this process use: the affinity set, capped by the CPU quota
-    # (more threads than the quota only time-slice: 256 threads under a 16-CPU quota ran 38% slower)
     threads = a.cpu_threads or max(1, min(affinity, int(quota_cpus + 0.5) if quota_cpus else affinity))
+    return threads, affinity, quota_cpus
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def cpu_baseline(a, man, eb, qbar, K):
+    """C restatement of the JVM path (OpenSSL BN Montgomery sliding window, 8-bit radix
+    fixed base = LOW_MEMORY_USE) on a bounded sample of the same ballots, on every host core
+    this process may run on, sized to about --cpu-seconds of work.  At N > 1 it runs on rank 0
+    after the timed steps and the final barrier, on rank 0's host sample (--cpu-max-ballots)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from eg_oracle_c import COracle
+    from electionguard.core import constants as C
+
+    threads, affinity, quota_cpus = cpu_threads(a)
     co = COracle(C.P, C.Q, C.G)
     co.set_key(K)
 
@@ -425,14 +503,7 @@ def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
     co.powp(bases, exps)
     per_core_modexp = nb_pow / (time.perf_counter() - t)
     quota = f", cgroup CPU quota {quota_cpus:.1f}" if quota_cpus else ", no cgroup CPU quota"
-    model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    model = cpu_model()
     return {
         "value": round(s / dt, 3),
         "unit": "ballots/s",
@@ -447,6 +518,10 @@ def cpu_baseline(a, man, eb, qbar, K, gpu_tally):
         "cgroup_quota_cpus": quota_cpus,
         "var_base_modexp_per_s_per_core": round(per_core_modexp, 1),
     }
+
+
+def full_pipeline(a, world, rank, local, dist):
+    raise SystemExit("--pipeline full: not built yet")
 
 
 if __name__ == "__main__":

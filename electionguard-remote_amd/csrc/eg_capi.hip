@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <array>
 #include <chrono>
 #include <condition_variable>
@@ -149,7 +150,7 @@ constexpr int kCtEncWindow = 6;
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_CRF, W_CAST, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_CRF, W_CAST, W_ANY, W_GATHER, W_NSLOT
 };
 
 struct eg_ctx {
@@ -162,7 +163,7 @@ struct eg_ctx {
   uint8_t* d_q = nullptr;
   uint8_t* d_qbar = nullptr;
   eg_fixed_base* gtab = nullptr;
-  eg_fixed_base* Ktab = nullptr;
+  eg_fixed_base* Ktab = nullptr;  // the current election key's radix table (keys.front().fb)
   uint32_t* d_gcomb = nullptr;  // Lim-Lee comb subset table of g (32 elements) for constant-time g^u
   uint32_t hash_fmt = EG_HASH_FIXED_WIDTH;  // Fiat-Shamir pre-image hex format (eg_ctx_set_hash_format)
   DevBuf ws[W_NSLOT];
@@ -171,14 +172,22 @@ struct eg_ctx {
   uint64_t* d_clk = nullptr;  // kClockRecs x 2 clock records of the open profile window
   size_t clk_used = 0;        // records handed out in this window
   uint32_t clk_used_last = 0, clk_dropped_last = 0;  // of the last closed window (eg_ctx_profile_clock)
-  uint8_t K_be[512];
+  uint8_t K_be[512];  // the current election key (keys.front().K)
+  // radix tables of the election keys seen on this ctx, most recently used first (a shared ctx may
+  // serve several keys: calls alternating between two keys reuse both tables instead of rebuilding
+  // one per call); each entry also holds the key's constant-time encryption table once built
+  struct KeyTabs {
+    std::array<uint8_t, 512> K;
+    eg_fixed_base* fb = nullptr;
+    eg_fixed_base* ct = nullptr;
+  };
+  std::vector<KeyTabs> keys;
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
   std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
   uint32_t ct_encrypt = 0;              // encryption on k_pow<F, true> with small CT tables (eg_ctx_set_ct_encrypt)
   int ct_window = kCtEncWindow;         // their radix width
-  eg_fixed_base *g_ct = nullptr, *K_ct = nullptr;  // their kCtEncWindow-bit tables of g and K
-  uint8_t K_ct_be[512];
+  eg_fixed_base* g_ct = nullptr;  // g's kCtEncWindow-bit table (K's live in keys[].ct)
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
   uint32_t sel_rows = 4;                // verifier selection jobs' comb: 4 = 4 rows x 3 blocks, 0 = 5 rows x 2 blocks (EG_SEL_COMB=52)
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
@@ -196,6 +205,9 @@ struct eg_ctx {
   // host-pointer verify: uploads of chunk k+1 on their own stream overlap chunk k's kernels
   hipStream_t copy = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
+  void* comm = nullptr;  // RCCL communicator of the multi-GPU exchange (eg_comm_init; eg_capi_comm.inc)
+  int comm_world = 1, comm_rank = 0;
+  int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
 
 static int ws_get(eg_ctx* c, Slot s, size_t bytes, void** out) {
@@ -696,6 +708,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
   if (const char* cr = getenv("EG_CT_ROWS")) c->ct_rows = (cr[0] == '5') ? 0u : 4u;
   if (const char* sc = getenv("EG_SEL_COMB")) c->sel_rows = (sc[0] == '5') ? 0u : 4u;
+  if (const char* tf = getenv("EG_TEST_FAIL_JOBS")) c->test_fail_jobs = atoi(tf);
   if (const char* cw = getenv("EG_CT_WINDOW")) c->ct_window = std::max(4, std::min((int)kCtMaxWindow, atoi(cw)));
   {
     int cus = 0, per_cu = 0;
@@ -739,16 +752,20 @@ extern "C" int eg_fixed_base_destroy(eg_fixed_base* fb) {
 }
 
 static void coalescer_stop(eg_ctx* c);  // eg_capi_coalesce.inc
+static int comm_destroy_locked(eg_ctx* c);  // eg_capi_comm.inc
 
 extern "C" int eg_ctx_destroy(eg_ctx* c) {
   if (!c) return EG_OK;
   coalescer_stop(c);  // drains pending per-element calls first
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  comm_destroy_locked(c);
   eg_fixed_base_destroy(c->gtab);
-  eg_fixed_base_destroy(c->Ktab);
+  for (auto& k : c->keys) {
+    eg_fixed_base_destroy(k.fb);
+    eg_fixed_base_destroy(k.ct);
+  }
   eg_fixed_base_destroy(c->g_ct);
-  eg_fixed_base_destroy(c->K_ct);
   for (auto& kv : c->share_keys) eg_fixed_base_destroy(kv.second);
   for (auto& b : c->ws)
     if (b.ptr) hipFree(b.ptr);
@@ -1051,6 +1068,7 @@ extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr
 
 #include "eg_capi_ballot.inc"
 #include "eg_capi_coalesce.inc"
+#include "eg_capi_comm.inc"
 
 // ------------------------------------------------------------------------------
 // device-pointer powP / fixed-base powP (asynchronous on the ctx stream): the
@@ -1060,12 +1078,9 @@ extern "C" int eg_ctx_profile_end(eg_ctx* c, double* ms, double* mm, double* sqr
 // ------------------------------------------------------------------------------
 static int identity_pow_jobs(eg_ctx* c, size_t n, bool fbonly, const uint32_t** out) {
   const std::string key = std::string(fbonly ? "fb/" : "pw/") + std::to_string(n);
-  if (c->cache.find(key) == c->cache.end() && c->cache.size() >= 64) {
-    HIPCHK(hipStreamSynchronize(c->stream));
-    for (auto& kv : c->cache) HIPCHK(hipFree(kv.second.ptr));
-    c->cache.clear();
-  }
   if (c->cache.find(key) == c->cache.end()) {
+    int rc = cache_bound(c);
+    if (rc) return rc;
     auto jobs = new_jobs(n);
     for (size_t i = 0; i < n; ++i) {
       uint32_t* J = &jobs[i * kJobWords];

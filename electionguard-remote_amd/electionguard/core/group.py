@@ -300,6 +300,134 @@ class GroupContext:
     def sync(self) -> None:
         native.check(self._lib, "eg_ctx_sync", self._lib.eg_ctx_sync(self._ctx))
 
+    # ---- device memory through this library's own HIP runtime (eg_dev_alloc, include/eg_hip.h) ----
+    def device_buffer(self, nbytes: int) -> "DeviceBuffer":
+        """``nbytes`` of HBM on this context's device (no other GPU framework in the process)."""
+        return DeviceBuffer(self, nbytes)
+
+    def device_empty(self, shape, dtype=np.uint8) -> "DeviceBuffer":
+        """An uninitialised device array of ``shape`` (bytes = prod(shape) x itemsize)."""
+        shape = (shape,) if isinstance(shape, int) else tuple(shape)
+        return DeviceBuffer(self, int(np.prod(shape)) * np.dtype(dtype).itemsize, shape, dtype)
+
+    def device_zeros(self, shape, dtype=np.uint8) -> "DeviceBuffer":
+        d = self.device_empty(shape, dtype)
+        d.zero()
+        return d
+
+    def to_device(self, a: np.ndarray) -> "DeviceBuffer":
+        """A device copy of the contiguous array ``a`` (its shape and dtype kept for download())."""
+        a = np.ascontiguousarray(a)
+        d = DeviceBuffer(self, a.nbytes, a.shape, a.dtype)
+        d.upload(a)
+        return d
+
+    def all_nonzero(self, d_flags: "DeviceBuffer", n: Optional[int] = None) -> bool:
+        """Every one of the first n flag bytes in HBM is non-zero (the verifier's ok_sel / ok_contest)."""
+        out = ctypes.c_int()
+        native.check(self._lib, "eg_all_nonzero_dev",
+                     self._lib.eg_all_nonzero_dev(self._ctx, d_flags.ptr, d_flags.nbytes if n is None else n,
+                                                  ctypes.byref(out)))
+        return bool(out.value)
+
+    # ---- the multi-GPU tally exchange on this context (RCCL inside libeg_hip, SURVEY §8e) ----
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = native.load()
+        b = bytearray(128)
+        native.check(lib, "eg_comm_unique_id", lib.eg_comm_unique_id(native.buf(b)))
+        return bytes(b)
+
+    def comm_init(self, uid: bytes, world: int, rank: int) -> None:
+        if len(uid) != 128:
+            raise ValueError("the RCCL unique id is 128 bytes")
+        native.check(self._lib, "eg_comm_init", self._lib.eg_comm_init(self._ctx, native.buf(uid), world, rank))
+        self._rank = rank
+
+    def comm_destroy(self) -> None:
+        native.check(self._lib, "eg_comm_destroy", self._lib.eg_comm_destroy(self._ctx))
+        self._rank = 0
+
+    def comm_all_valid(self, ok: bool) -> bool:
+        out = ctypes.c_int()
+        native.check(self._lib, "eg_comm_all_valid",
+                     self._lib.eg_comm_all_valid(self._ctx, 1 if ok else 0, ctypes.byref(out)))
+        return bool(out.value)
+
+    def tally_allgather_fold(self, d_parts: "DeviceBuffer", nparts: int, n: int, root: int = 0) -> Optional[np.ndarray]:
+        """Fold every rank's nparts x n partial-tally elements (512-B rows in HBM) mod p on ``root``
+        (eg_tally_allgather_fold: one RCCL all-gather + the k_prod tree); -> (n, 512) on root, None
+        elsewhere.  Without comm_init the local parts are folded."""
+        out = np.empty((n, P_BYTES), dtype=np.uint8)
+        native.check(self._lib, "eg_tally_allgather_fold",
+                     self._lib.eg_tally_allgather_fold(self._ctx, d_parts.ptr, nparts, n, root, _ptr(out)))
+        return out if self._comm_rank() == root else None
+
+    def _comm_rank(self) -> int:
+        return getattr(self, "_rank", 0)
+
+
+class DeviceBuffer:
+    """HBM allocated through libeg_hip (eg_dev_alloc): ``ptr`` is the device address the *_dev
+    entry points take.  Freed by ``free()`` (after the ctx stream drains) or on collection."""
+
+    def __init__(self, group: GroupContext, nbytes: int, shape=None, dtype=np.uint8):
+        self.group = group
+        self.nbytes = int(nbytes)
+        self.shape = tuple(shape) if shape is not None else (self.nbytes,)
+        self.dtype = np.dtype(dtype)
+        h = ctypes.c_void_p()
+        native.check(group._lib, "eg_dev_alloc", group._lib.eg_dev_alloc(group.handle, self.nbytes, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def ptr(self) -> int:
+        return (self._h.value or 0) + getattr(self, "_off", 0)
+
+    def __getitem__(self, sl: slice) -> "DeviceBuffer":
+        """A view of rows [start, stop) along the first axis (shares the memory; never frees it)."""
+        if not isinstance(sl, slice) or sl.step not in (None, 1):
+            raise TypeError("device buffers slice contiguous rows only")
+        start, stop, _ = sl.indices(self.shape[0])
+        stop = max(start, stop)
+        row = self.nbytes // max(self.shape[0], 1)
+        v = DeviceBuffer.__new__(DeviceBuffer)
+        v.group, v.dtype = self.group, self.dtype
+        v.shape = (stop - start,) + self.shape[1:]
+        v.nbytes = row * (stop - start)
+        v._h, v._off, v._owner = self._h, getattr(self, "_off", 0) + row * start, self
+        return v
+
+    def upload(self, a: np.ndarray) -> None:
+        a = np.ascontiguousarray(a)
+        if a.nbytes != self.nbytes:
+            raise ValueError(f"upload of {a.nbytes} B into a {self.nbytes}-B buffer")
+        native.check(self.group._lib, "eg_memcpy_htod",
+                     self.group._lib.eg_memcpy_htod(self.group.handle, self.ptr, _ptr(a), a.nbytes))
+
+    def download(self) -> np.ndarray:
+        out = np.empty(self.shape, dtype=self.dtype)
+        native.check(self.group._lib, "eg_memcpy_dtoh",
+                     self.group._lib.eg_memcpy_dtoh(self.group.handle, _ptr(out), self.ptr, self.nbytes))
+        return out
+
+    def zero(self) -> None:
+        native.check(self.group._lib, "eg_memset_dev", self.group._lib.eg_memset_dev(self.group.handle, self.ptr, 0,
+                                                                                     self.nbytes))
+
+    def free(self) -> None:
+        if getattr(self, "_owner", None) is not None:  # a view: the owner frees the memory
+            return
+        if getattr(self, "_h", None) and self._h.value and getattr(self.group, "_ctx", None):
+            self.group._lib.eg_dev_free(self.group.handle, self._h)
+        self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.free()
+        except Exception:
+            pass
+
 
 class FixedBase:
     """Accelerated base (``acceleratePow`` / PowRadix): radix table on the device."""

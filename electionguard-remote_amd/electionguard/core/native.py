@@ -26,6 +26,8 @@ EXPORTED = [
     "eg_trustee_decrypt_batch", "eg_verify_shares", "eg_clock_median",
     "eg_ctx_set_coalescing", "eg_powp_submit", "eg_gpowp_submit", "eg_multp_submit", "eg_ticket_wait",
     "eg_powp_one", "eg_gpowp_one", "eg_multp_one", "eg_ctx_set_ct_encrypt",
+    "eg_dev_alloc", "eg_dev_free", "eg_memcpy_htod", "eg_memcpy_dtoh", "eg_memset_dev", "eg_all_nonzero_dev",
+    "eg_comm_unique_id", "eg_comm_init", "eg_comm_destroy", "eg_comm_all_valid", "eg_tally_allgather_fold",
 ]
 
 
@@ -89,6 +91,17 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_multp_one": ([P, P, P, P], I),
         "eg_trustee_decrypt_batch": ([P, P, P, P, P, S, P, P], I),
         "eg_verify_shares": ([P, P, P, P, P, P, S, P], I),
+        "eg_dev_alloc": ([P, S, ctypes.POINTER(c_vp)], I),
+        "eg_dev_free": ([P, P], I),
+        "eg_memcpy_htod": ([P, P, P, S], I),
+        "eg_memcpy_dtoh": ([P, P, P, S], I),
+        "eg_memset_dev": ([P, P, I, S], I),
+        "eg_all_nonzero_dev": ([P, P, S, ctypes.POINTER(I)], I),
+        "eg_comm_unique_id": ([P], I),
+        "eg_comm_init": ([P, P, I, I], I),
+        "eg_comm_destroy": ([P], I),
+        "eg_comm_all_valid": ([P, I, ctypes.POINTER(I)], I),
+        "eg_tally_allgather_fold": ([P, P, S, S, I, P], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)

@@ -6,6 +6,14 @@ rank): one all-gather over RCCL/xGMI, then a mod-p fold on rank 0 (RCCL has no
 modular-multiply reduction op).  Verdicts are combined with an all-reduce(min).
 Trustees are NOT sharded: each remote DecryptingTrustee is its own process with its own
 GPU (replicas only, separate trust domains).
+
+The exchange runs inside libeg_hip.so (``TallyExchange`` in "rccl" mode: eg_comm_init /
+eg_comm_all_valid / eg_tally_allgather_fold on the context's stream and HIP runtime), so a
+rank process holds one HIP runtime and never passes device memory to another framework.  A
+host process group (torch.distributed over gloo: CPU only, it never touches the GPU) carries
+the control traffic: the RCCL unique id, barriers and the max-over-ranks step time.  Mode
+"gloo" keeps the whole exchange on the host (every rank may then share one GPU: the
+single-GPU rehearsal of the N > 1 path, and the CPU tests).
 """
 from __future__ import annotations
 
@@ -27,7 +35,8 @@ def _host_collectives(dist) -> bool:
     return dist.get_backend() == "gloo"
 
 
-def all_valid(dist, ok: bool, device) -> bool:
+def all_valid(dist, ok: bool, device=None) -> bool:
+    """min over ranks of ok through the torch process group (host tensors under gloo)."""
     import torch
 
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
@@ -40,11 +49,13 @@ def all_valid(dist, ok: bool, device) -> bool:
 
 def gather_fold_tally(dist, local_tally, fold: Callable[[np.ndarray, int, int], np.ndarray],
                       dst: int = 0) -> Optional[np.ndarray]:
-    """All-gather (n_real, 2, 512) uint8 partial tallies from every rank and fold them
-    mod p on `dst` with fold(elems (groups*world, 512), groups, world) -> (groups, 512)
-    (GroupContext.prodP_groups on the GPU in production)."""
+    """All-gather (n_real, 2, 512) uint8 partial tallies (a numpy array or torch tensor) from every
+    rank and fold them mod p on `dst` with fold(elems (groups*world, 512), groups, world) ->
+    (groups, 512) (GroupContext.prodP_groups on the GPU in production)."""
     import torch
 
+    if isinstance(local_tally, np.ndarray):
+        local_tally = torch.from_numpy(np.ascontiguousarray(local_tally))
     world = dist.get_world_size() if (dist is not None and dist.is_initialized()) else 1
     if world == 1:
         return local_tally.cpu().numpy()
@@ -62,3 +73,68 @@ def gather_fold_tally(dist, local_tally, fold: Callable[[np.ndarray, int, int], 
     n_real = parts.shape[1]
     g = np.ascontiguousarray(np.transpose(parts, (1, 2, 0, 3))).reshape(-1, 512)
     return fold(g, n_real * 2, world).reshape(n_real, 2, 512)
+
+
+def share_comm_id(dist, rank: int, make_id: Callable[[], bytes], src: int = 0) -> bytes:
+    """Rank `src` makes the 128-byte RCCL unique id (eg_comm_unique_id) and every rank of the host
+    process group receives it (broadcast over gloo, before any rank touches RCCL)."""
+    box = [make_id() if rank == src else None]
+    dist.broadcast_object_list(box, src=src)
+    uid = box[0]
+    if not isinstance(uid, (bytes, bytearray)) or len(uid) != 128:
+        raise RuntimeError("bad RCCL unique id from rank %d" % src)
+    return bytes(uid)
+
+
+def max_over_ranks(dist, x: float) -> float:
+    """max of a host float over the host process group (the step time every rank measured)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(x)
+    import torch
+
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+class TallyExchange:
+    """The per-step exchange of the sharded verify + tally for one rank.
+
+    mode "rccl": libeg_hip's RCCL communicator on the group's context (the id travels over
+    ``dist``, the host process group); the verdict is an RCCL all-reduce(min) and the tally one
+    ncclAllGather plus the k_prod fold on rank 0's GPU (eg_tally_allgather_fold).
+    mode "gloo": the tally comes back to the host and travels over ``dist`` (gloo), rank 0 folds
+    it on its GPU (prodP_groups); every rank may share one GPU.
+    world 1: the local tally, through the same fold entry point (no communicator)."""
+
+    def __init__(self, group, dist, world: int, rank: int, mode: str = "rccl"):
+        if mode not in ("rccl", "gloo"):
+            raise ValueError(f"unknown exchange mode {mode!r}")
+        self.group, self.dist, self.world, self.rank, self.mode = group, dist, world, rank, mode
+        if world > 1 and mode == "rccl":
+            uid = share_comm_id(dist, rank, group.comm_unique_id)
+            group.comm_init(uid, world, rank)
+
+    @property
+    def collective(self) -> str:
+        return "RCCL (libeg_hip)" if self.world == 1 or self.mode == "rccl" else "gloo (host)"
+
+    def all_valid(self, ok: bool) -> bool:
+        if self.world == 1:
+            return bool(ok)
+        if self.mode == "rccl":
+            return self.group.comm_all_valid(ok)
+        return all_valid(self.dist, ok)
+
+    def fold(self, d_tally, n_real: int) -> Optional[np.ndarray]:
+        """d_tally: this rank's (n_real, 2, 512) partial tally in HBM (a DeviceBuffer) ->
+        the folded (n_real, 2, 512) tally on rank 0, None on the others."""
+        if self.world == 1 or self.mode == "rccl":
+            out = self.group.tally_allgather_fold(d_tally, 1, n_real * 2, 0)
+            return None if out is None else out.reshape(n_real, 2, 512)
+        local = d_tally.download().reshape(n_real, 2, 512)
+        return gather_fold_tally(self.dist, local, self.group.prodP_groups)
+
+    def close(self) -> None:
+        if self.world > 1 and self.mode == "rccl":
+            self.group.comm_destroy()

@@ -516,3 +516,98 @@ JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_ticketWait(JNIEnv* env, jcla
     (*env)->SetByteArrayRegion(env, out, 0, EG_P_BYTES, (const jbyte*)jt->out);
   free(jt);
 }
+
+/* ---------------------------------------------------------------- device memory (eg_dev_*) */
+/* HBM of the ctx's device through libeg_hip's own runtime; handles are device addresses (jlong). */
+
+JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_devAlloc(JNIEnv* env, jclass cls, jlong ctx, jlong bytes) {
+  if (neg(env, bytes, "bytes < 0")) return 0;
+  void* d = NULL;
+  if (check_rc(env, eg_dev_alloc((eg_ctx*)(intptr_t)ctx, (size_t)bytes, &d))) return 0;
+  return (jlong)(intptr_t)d;
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_devFree(JNIEnv* env, jclass cls, jlong ctx, jlong d) {
+  check_rc(env, eg_dev_free((eg_ctx*)(intptr_t)ctx, (void*)(intptr_t)d));
+}
+
+/* src[srcOff, srcOff + bytes) -> device dDst */
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_memcpyHtoD(JNIEnv* env, jclass cls, jlong ctx, jlong dDst,
+                                                               jbyteArray src, jlong srcOff, jlong bytes) {
+  if (neg(env, srcOff, "srcOff < 0") || neg(env, bytes, "bytes < 0") ||
+      need_len(env, src, (size_t)srcOff + (size_t)bytes, 0, "src shorter than srcOff + bytes"))
+    return;
+  int pinned = 1;
+  uint8_t* s = PIN(src);
+  const int rc = CALL_IF_PINNED(eg_memcpy_htod((eg_ctx*)(intptr_t)ctx, (void*)(intptr_t)dDst, s + srcOff, (size_t)bytes));
+  UNPIN_IN(src, s);
+  check_rc(env, rc);
+}
+
+/* device dSrc -> dst[dstOff, dstOff + bytes) */
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_memcpyDtoH(JNIEnv* env, jclass cls, jlong ctx, jbyteArray dst,
+                                                               jlong dstOff, jlong dSrc, jlong bytes) {
+  if (neg(env, dstOff, "dstOff < 0") || neg(env, bytes, "bytes < 0") ||
+      need_len(env, dst, (size_t)dstOff + (size_t)bytes, 0, "dst shorter than dstOff + bytes"))
+    return;
+  int pinned = 1;
+  uint8_t* d = PIN(dst);
+  const int rc = CALL_IF_PINNED(eg_memcpy_dtoh((eg_ctx*)(intptr_t)ctx, d + dstOff, (const void*)(intptr_t)dSrc, (size_t)bytes));
+  UNPIN_OUT(dst, d);
+  check_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_memsetDev(JNIEnv* env, jclass cls, jlong ctx, jlong d, jint value,
+                                                              jlong bytes) {
+  if (neg(env, bytes, "bytes < 0")) return;
+  check_rc(env, eg_memset_dev((eg_ctx*)(intptr_t)ctx, (void*)(intptr_t)d, value, (size_t)bytes));
+}
+
+JNIEXPORT jboolean JNICALL Java_electionguard_gpu_EgHip_allNonzeroDev(JNIEnv* env, jclass cls, jlong ctx, jlong dFlags,
+                                                                      jlong n) {
+  if (neg(env, n, "n < 0")) return JNI_FALSE;
+  int all = 0;
+  if (check_rc(env, eg_all_nonzero_dev((eg_ctx*)(intptr_t)ctx, (const uint8_t*)(intptr_t)dFlags, (size_t)n, &all)))
+    return JNI_FALSE;
+  return all ? JNI_TRUE : JNI_FALSE;
+}
+
+/* ---------------------------------------------------------------- multi-GPU tally exchange (eg_comm_*) */
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_commUniqueId(JNIEnv* env, jclass cls, jbyteArray out128) {
+  if (need_len(env, out128, EG_COMM_ID_BYTES, 0, "out: 128 bytes")) return;
+  uint8_t id[EG_COMM_ID_BYTES];
+  if (check_rc(env, eg_comm_unique_id(id))) return;
+  (*env)->SetByteArrayRegion(env, out128, 0, EG_COMM_ID_BYTES, (const jbyte*)id);
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_commInit(JNIEnv* env, jclass cls, jlong ctx, jbyteArray id128,
+                                                             jint world, jint rank) {
+  uint8_t id[EG_COMM_ID_BYTES];
+  if (get_fixed(env, id128, EG_COMM_ID_BYTES, id, "id: 128 bytes")) return;
+  check_rc(env, eg_comm_init((eg_ctx*)(intptr_t)ctx, id, world, rank));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_commDestroy(JNIEnv* env, jclass cls, jlong ctx) {
+  check_rc(env, eg_comm_destroy((eg_ctx*)(intptr_t)ctx));
+}
+
+JNIEXPORT jboolean JNICALL Java_electionguard_gpu_EgHip_commAllValid(JNIEnv* env, jclass cls, jlong ctx, jboolean ok) {
+  int all = 0;
+  if (check_rc(env, eg_comm_all_valid((eg_ctx*)(intptr_t)ctx, ok ? 1 : 0, &all))) return JNI_FALSE;
+  return all ? JNI_TRUE : JNI_FALSE;
+}
+
+/* out: n x 512 bytes on the root (may be null on the other ranks) */
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_tallyAllgatherFold(JNIEnv* env, jclass cls, jlong ctx, jlong dParts,
+                                                                       jlong nparts, jlong n, jint root, jbyteArray out) {
+  if (neg(env, nparts, "nparts < 0") || neg(env, n, "n < 0") ||
+      need_len(env, out, (size_t)n * EG_P_BYTES, 1, "out: n x 512 bytes"))
+    return;
+  int pinned = 1;
+  uint8_t* o = PIN(out);
+  const int rc = CALL_IF_PINNED(eg_tally_allgather_fold((eg_ctx*)(intptr_t)ctx, (const uint8_t*)(intptr_t)dParts,
+                                                        (size_t)nparts, (size_t)n, root, o));
+  UNPIN_OUT(out, o);
+  check_rc(env, rc);
+}

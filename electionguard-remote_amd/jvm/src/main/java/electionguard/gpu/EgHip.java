@@ -128,4 +128,32 @@ public final class EgHip {
   public static native long multpSubmit(long ctx, byte[] a512, byte[] b512);
 
   public static native void ticketWait(long ticket, byte[] out512);
+
+  // ---- device memory through libeg_hip's own HIP runtime (eg_dev_*): handles are HBM addresses ----
+  public static native long devAlloc(long ctx, long bytes);
+
+  public static native void devFree(long ctx, long d);
+
+  public static native void memcpyHtoD(long ctx, long dDst, byte[] src, long srcOff, long bytes);
+
+  public static native void memcpyDtoH(long ctx, byte[] dst, long dstOff, long dSrc, long bytes);
+
+  public static native void memsetDev(long ctx, long d, int value, long bytes);
+
+  /** Every one of n flag bytes in HBM non-zero (the verifier's ok_sel / ok_contest). */
+  public static native boolean allNonzeroDev(long ctx, long dFlags, long n);
+
+  // ---- multi-GPU tally exchange (SURVEY 8e): RCCL inside libeg_hip, one rank per GPU ----
+  /** Rank 0 makes the 128-byte id; the caller sends it to every rank (any host channel). */
+  public static native void commUniqueId(byte[] out128);
+
+  public static native void commInit(long ctx, byte[] id128, int world, int rank);
+
+  public static native void commDestroy(long ctx);
+
+  /** min over ranks of ok (the verdict all-reduce). */
+  public static native boolean commAllValid(long ctx, boolean ok);
+
+  /** Every rank's nparts x n partial-tally rows (HBM, 512 B each) folded mod p into out on root. */
+  public static native void tallyAllgatherFold(long ctx, long dParts, long nparts, long n, int root, byte[] out);
 }

@@ -142,6 +142,13 @@ int eg_multinv_batch(eg_ctx* ctx, const uint8_t* a_be, uint8_t* out_be, size_t n
  * spoiled ones are decrypted individually, RunRemoteDecryptor.java:264-269).
  * Outputs: ok_sel[nballots*nsel], ok_contest[nballots*ncontest] (1 = valid),
  * tally_be[ncontest*(spc-placeholders)*2*512] (may be NULL; all ones for no cast ballot).
+ * A contest's verdict includes the validity of its message (A, B) = (prod alpha, prod beta),
+ * decided from its selections: every alpha and beta must be in range and a valid residue
+ * (x^q = 1).  This is a deliberate, documented choice: a contest whose
+ * selections hold two non-residue alphas with a residue product is REJECTED here, while a check
+ * of A^q = 1 alone would accept its constant proof; the ballot's verdict is the same either way
+ * (the selections fail), and the oracles apply the same rule (tests/test_gpu_golden.py,
+ * test_gpu_rejects_contest_whose_selections_are_invalid).
  * The key is set under the ctx lock for the call (a matching table is reused; a different K
  * rebuilds it at the window width of the ctx's current table, see eg_set_election_key). */
 int eg_verify_ballots(eg_ctx* ctx, const uint8_t K_be[EG_P_BYTES], const uint8_t qbar_be[EG_Q_BYTES],
@@ -222,6 +229,37 @@ int eg_powp_one(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], const uint8_t ex
 int eg_gpowp_one(eg_ctx* ctx, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES]);
 int eg_multp_one(eg_ctx* ctx, const uint8_t a_be[EG_P_BYTES], const uint8_t b_be[EG_P_BYTES],
                  uint8_t out_be[EG_P_BYTES]);
+
+/* ---- device memory on the ctx's device (no reference counterpart: it lets a caller keep ballots
+ * resident in HBM through this library alone, so its process runs ONE HIP runtime; bench.py) ----
+ * Copies are ordered after every call queued on the ctx before them and return when complete;
+ * eg_dev_free waits for the ctx stream first.  eg_all_nonzero_dev: *all = 1 iff every one of the
+ * n flags (e.g. eg_verify_ballots_dev's d_ok_sel) is non-zero. */
+int eg_dev_alloc(eg_ctx* ctx, size_t bytes, void** d_out);
+int eg_dev_free(eg_ctx* ctx, void* d);
+int eg_memcpy_htod(eg_ctx* ctx, void* d_dst, const void* src, size_t bytes);
+int eg_memcpy_dtoh(eg_ctx* ctx, void* dst, const void* d_src, size_t bytes);
+int eg_memset_dev(eg_ctx* ctx, void* d, int value, size_t bytes);
+int eg_all_nonzero_dev(eg_ctx* ctx, const uint8_t* d_flags, size_t n, int* all);
+
+/* ---- multi-GPU tally exchange (ballots sharded over the node's GPUs, one process
+ * per GPU, partial tallies all-gathered over RCCL/xGMI and folded mod p on one GPU; the
+ * reference's RunRemoteWorkflowTest.java:151 accumulates the whole tally in one process) ----
+ * RCCL (librccl.so.1, dlopen'd on first use) runs on the ctx's stream and HIP runtime.
+ * eg_comm_unique_id: rank 0 makes the 128-byte id, the caller distributes it (any host channel);
+ * eg_comm_init: every rank calls it with the same id (collective); one communicator per ctx.
+ * eg_comm_all_valid: *all_ok = min over ranks of local_ok (the verdict all-reduce).
+ * eg_tally_allgather_fold: every rank passes nparts partial tallies of n elements (d_parts_be,
+ * nparts x n x 512 B big-endian in HBM); root receives out_be[k] = product over every rank and
+ * part of element k mod p (n x 512 B, host; may be NULL on the other ranks).  One ncclAllGather
+ * plus the k_prod tree on root's GPU.  Without eg_comm_init it folds the local parts alone. */
+#define EG_COMM_ID_BYTES 128
+int eg_comm_unique_id(uint8_t id[EG_COMM_ID_BYTES]);
+int eg_comm_init(eg_ctx* ctx, const uint8_t id[EG_COMM_ID_BYTES], int world, int rank);
+int eg_comm_destroy(eg_ctx* ctx);
+int eg_comm_all_valid(eg_ctx* ctx, int local_ok, int* all_ok);
+int eg_tally_allgather_fold(eg_ctx* ctx, const uint8_t* d_parts_be, size_t nparts, size_t n, int root,
+                            uint8_t* out_be);
 
 #ifdef __cplusplus
 }

@@ -20,16 +20,9 @@ def oracle_group():
     return O.production_group()
 
 
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first(request):
-    # torch bundles its own libamdhip64.so.7: it must bring up its HIP runtime BEFORE
-    # libeg_hip.so pulls in the system one, or torch sees no GPU (tests that hand torch
-    # device tensors to the C ABI need both).  bench.py has the same order.  Session-wide, so
-    # no test order (a fixture opening a context directly) can load the library first.
-    if any(item.get_closest_marker("gpu") for item in request.session.items):
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.init()
+# No GPU framework besides libeg_hip.so is brought up in the test process: device buffers come from
+# the library itself (GroupContext.device_buffer / to_device, eg_dev_alloc), so the process holds
+# one HIP runtime (torch is imported by the CPU tests for its gloo process group only).
 
 
 @pytest.fixture(scope="session")

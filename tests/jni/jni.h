@@ -15,6 +15,8 @@ typedef int32_t jint;
 typedef int64_t jlong;
 typedef int8_t jbyte;
 typedef uint8_t jboolean;
+#define JNI_FALSE 0
+#define JNI_TRUE 1
 typedef double jdouble;
 typedef jint jsize;
 

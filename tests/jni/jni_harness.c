@@ -315,6 +315,44 @@ int main(void) {
     EXPECT_MSG("null");
   }
 
+  /* ---- device memory and the tally exchange ---- */
+  Java_electionguard_gpu_EgHip_devAlloc(env, C, N0, -1);
+  EXPECT("devAlloc bytes < 0", IAE);
+  Java_electionguard_gpu_EgHip_devAlloc(env, C, N0, 64);
+  EXPECT("devAlloc(0)", AE);
+  EXPECT_MSG("null");
+  Java_electionguard_gpu_EgHip_devFree(env, C, N0, 0);
+  EXPECT("devFree(0)", AE);
+  Java_electionguard_gpu_EgHip_memcpyHtoD(env, C, N0, 0, sh, 4, 8);
+  EXPECT("memcpyHtoD past the array", IAE);
+  Java_electionguard_gpu_EgHip_memcpyHtoD(env, C, N0, 0, p, 0, 512);
+  EXPECT("memcpyHtoD(0)", AE);
+  Java_electionguard_gpu_EgHip_memcpyDtoH(env, C, N0, sh, -1, 0, 4);
+  EXPECT("memcpyDtoH dstOff < 0", IAE);
+  Java_electionguard_gpu_EgHip_memcpyDtoH(env, C, N0, p, 0, 0, 512);
+  EXPECT("memcpyDtoH(0)", AE);
+  Java_electionguard_gpu_EgHip_memsetDev(env, C, N0, 0, 0, 16);
+  EXPECT("memsetDev(0)", AE);
+  Java_electionguard_gpu_EgHip_allNonzeroDev(env, C, N0, 0, 16);
+  EXPECT("allNonzeroDev(0)", AE);
+  Java_electionguard_gpu_EgHip_commUniqueId(env, C, sh);
+  EXPECT("commUniqueId short out", IAE);
+  Java_electionguard_gpu_EgHip_commInit(env, C, N0, sh, 2, 0);
+  EXPECT("commInit short id", IAE);
+  {
+    Obj* id = bytes(128);
+    Java_electionguard_gpu_EgHip_commInit(env, C, N0, id, 2, 0);
+    EXPECT("commInit(0)", AE);
+  }
+  Java_electionguard_gpu_EgHip_commDestroy(env, C, N0);
+  EXPECT("commDestroy(0)", AE);
+  Java_electionguard_gpu_EgHip_commAllValid(env, C, N0, 1);
+  EXPECT("commAllValid(0)", AE);
+  Java_electionguard_gpu_EgHip_tallyAllgatherFold(env, C, N0, 0, 1, 2, 0, p);
+  EXPECT("tallyAllgatherFold short out", IAE);
+  Java_electionguard_gpu_EgHip_tallyAllgatherFold(env, C, N0, 0, 1, 2, 0, b2);
+  EXPECT("tallyAllgatherFold(0)", AE);
+
   printf("jni harness: %d checks, %d errors, %d pins, %d releases\n", g_checks, g_errors, g_pins, g_unpins);
   return g_errors || g_pins != g_unpins ? 1 : 0;
 }

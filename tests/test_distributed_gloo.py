@@ -121,25 +121,81 @@ def test_bench_config_names():
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
     from bench import config_name
     assert config_name(4, 5, 10_000, 1) == "configs[1]"
-    assert config_name(4, 5, 125_000, 8).startswith("configs[2]")
+    assert config_name(4, 5, 125_000, 8).startswith("configs[2] (1M ballots over 8 GPUs")
+    assert config_name(4, 5, 125_000, 2).startswith("configs[2] per-GPU shard")
     assert config_name(4, 5, 1_000_000, 1).startswith("configs[2]")
     assert config_name(4, 5, 10_000, 8) == "configs[1] shape (4x5), 10000 ballots per GPU x 8 GPUs"
     assert config_name(4, 5, 2_000, 2).startswith("configs[1] shape")
     assert config_name(20, 5, 10_000, 4).startswith("configs[4] shape")
     assert config_name(20, 5, 250_000, 4).startswith("configs[4] (1M ballots")
+    assert config_name(20, 5, 125_000, 1).startswith("configs[4] per-GPU shard")
 
 
 def test_bench_default_workload_per_gpu_count():
-    """N = 1 measures configs[1] (10k ballots); N > 1 measures configs[2] (1M ballots over the
-    node, 1M // N per rank), without any flag."""
+    """N = 1 measures configs[1] (10k ballots); N > 1 measures configs[2]'s per-GPU shard (125k
+    ballots per rank: weak scaling, N = 8 is configs[2]'s 1M ballots) without any flag;
+    --pipeline full runs configs[4]'s 125k-ballot shard of the 20 x (5+1) manifest at every N."""
     import sys
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-    from bench import config_name, default_ballots
+    from bench import config_name, default_ballots, parse
     assert default_ballots(1) == 10_000 and config_name(4, 5, default_ballots(1), 1) == "configs[1]"
     for n in (2, 4, 8):
-        assert default_ballots(n) * n == 1_000_000
-        assert config_name(4, 5, default_ballots(n), n) == f"configs[2] (1M ballots over {n} GPUs)"
+        assert default_ballots(n) == 125_000
+    assert config_name(4, 5, default_ballots(8), 8) == "configs[2] (1M ballots over 8 GPUs)"
+    a = parse(["--pipeline", "full"])
+    assert (a.contests, a.ballots) == (20, 125_000)
+    assert config_name(a.contests, a.selections, a.ballots, 8).startswith("configs[4] (1M ballots")
+
+
+def test_bench_line_at_world_2_has_cpu_baseline(tmp_path):
+    """bench.py's N > 1 tail (bench.report) on 2 gloo ranks: after the barrier rank 0 times the CPU
+    port on its host sample, and its line carries cpu_baseline (kind port, cores stated) and a
+    non-null vs_baseline = value / cpu_baseline.value."""
+    import json
+    from pathlib import Path
+    from electionguard.launch import run_ranks
+    child = Path(__file__).resolve().parent / "_bench_report_child.py"
+    out = tmp_path / "line.json"
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    assert run_ranks(str(child), [str(out)], 2, timeout=240, env=env) == 0
+    d = json.loads(out.read_text())
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and "verdicts all valid: True" in cb["sample"]
+    assert d["vs_baseline"] is not None and abs(d["vs_baseline"] - d["value"] / cb["value"]) < 0.01 * d["vs_baseline"] + 0.01
+    assert "cpu_baseline.value" in d["vs_baseline_basis"]
+
+
+def test_comm_id_rendezvous_over_gloo():
+    """The RCCL unique id (eg_comm_unique_id on rank 0) reaches every rank of the host process
+    group unchanged (electionguard.distributed.share_comm_id, the rendezvous TallyExchange uses
+    before eg_comm_init); a stand-in id is used here (no GPU)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_id_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = bytes(range(128))
+    assert [r for r, _ in got] == [0, 1, 2] and all(uid == want for _, uid in got)
+
+
+def _id_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from electionguard.distributed import share_comm_id
+
+    def make():
+        assert rank == 0, "only rank 0 makes the id"
+        return bytes(range(128))
+
+    q.put((rank, share_comm_id(dist, rank, make)))
+    dist.destroy_process_group()
 
 
 def test_launcher_fails_fast_when_a_rank_dies(tmp_path):

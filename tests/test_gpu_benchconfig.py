@@ -34,7 +34,6 @@ def bench_batch(group):
 
 
 def test_bench_config_verdicts_tally_and_device_path(group, bench_batch):
-    import torch
     from eg_oracle_c import COracle
     from electionguard.ballot import Verifier
     man, key, K, qbar, votes, eb = bench_batch
@@ -60,16 +59,15 @@ def test_bench_config_verdicts_tally_and_device_path(group, bench_batch):
                 acc = acc * int.from_bytes(eb.cts[b, i, c].tobytes(), "big") % p
             assert int.from_bytes(tally[s, c].tobytes(), "big") == acc, (s, c)
     # the device-pointer path bench.py times
-    dev = torch.device("cuda", 0)
-    d_cts, d_rp, d_cp = (torch.from_numpy(a).to(dev) for a in (eb.cts, eb.rproof, eb.cproof))
-    d_oks = torch.zeros((eb.n, man.nsel), dtype=torch.uint8, device=dev)
-    d_okc = torch.zeros((eb.n, man.n_contests), dtype=torch.uint8, device=dev)
-    d_tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-    V.verify_device(d_cts.data_ptr(), d_rp.data_ptr(), d_cp.data_ptr(), eb.n, d_oks.data_ptr(), d_okc.data_ptr(),
-                    d_tal.data_ptr())
+    d_cts, d_rp, d_cp = (group.to_device(a) for a in (eb.cts, eb.rproof, eb.cproof))
+    d_oks = group.device_zeros((eb.n, man.nsel))
+    d_okc = group.device_zeros((eb.n, man.n_contests))
+    d_tal = group.device_zeros((man.n_real, 2, 512))
+    V.verify_device(d_cts.ptr, d_rp.ptr, d_cp.ptr, eb.n, d_oks.ptr, d_okc.ptr,
+                    d_tal.ptr)
     group.sync()
-    assert bool(d_oks.all()) and bool(d_okc.all())
-    assert np.array_equal(d_tal.cpu().numpy(), tally)
+    assert group.all_nonzero(d_oks) and group.all_nonzero(d_okc)
+    assert np.array_equal(d_tal.download(), tally)
 
 
 def test_bench_config_single_bit_tamper(group, bench_batch):

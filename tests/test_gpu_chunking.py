@@ -130,7 +130,6 @@ def test_three_streamed_chunks(group):
 def test_device_encryption_matches_host(group):
     """eg_encrypt_ballots_dev (inputs and outputs in HBM, two chunks) writes exactly the
     bytes of the host-pointer eg_encrypt_ballots for the same injected nonces."""
-    import torch
     from electionguard.ballot import (ElectionKey, Manifest, batch_encryption, batch_encryption_device,
                                       random_scalars, random_votes)
     from electionguard.keyceremony import key_ceremony
@@ -143,17 +142,15 @@ def test_device_encryption_matches_host(group):
     sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
     cn = random_scalars(rng, (nb, man.n_contests), group.q)
     eb = batch_encryption(group, key, 555, man, votes, sn, cn)
-    d = torch.device("cuda", 0)
-    dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(d) for x in (votes, sn, cn))
-    oc = torch.empty(eb.cts.shape, dtype=torch.uint8, device=d)
-    orp = torch.empty(eb.rproof.shape, dtype=torch.uint8, device=d)
-    ocp = torch.empty(eb.cproof.shape, dtype=torch.uint8, device=d)
-    torch.cuda.synchronize()
-    batch_encryption_device(group, key, 555, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(), oc.data_ptr(),
-                            orp.data_ptr(), ocp.data_ptr())
-    assert np.array_equal(oc.cpu().numpy(), eb.cts)
-    assert np.array_equal(orp.cpu().numpy(), eb.rproof)
-    assert np.array_equal(ocp.cpu().numpy(), eb.cproof)
+    dv, dsn, dcn = (group.to_device(np.ascontiguousarray(x)) for x in (votes, sn, cn))
+    oc = group.device_empty(eb.cts.shape)
+    orp = group.device_empty(eb.rproof.shape)
+    ocp = group.device_empty(eb.cproof.shape)
+    batch_encryption_device(group, key, 555, man, nb, dv.ptr, dsn.ptr, dcn.ptr, oc.ptr,
+                            orp.ptr, ocp.ptr)
+    assert np.array_equal(oc.download(), eb.cts)
+    assert np.array_equal(orp.download(), eb.rproof)
+    assert np.array_equal(ocp.download(), eb.cproof)
 
 
 def test_host_pointer_encryption_equals_device_resident_with_wide_contests(group):
@@ -162,7 +159,6 @@ def test_host_pointer_encryption_equals_device_resident_with_wide_contests(group
     chunk 0's outputs are still being copied back (the contest proofs of output
     set 0 used to share that buffer).  The host-pointer bytes must equal the device-resident
     encryption's, which has no copy-back overlap."""
-    import torch
     from electionguard.ballot import (ElectionKey, Manifest, batch_encryption, batch_encryption_device,
                                       random_scalars, random_votes)
     from electionguard.keyceremony import key_ceremony
@@ -175,17 +171,15 @@ def test_host_pointer_encryption_equals_device_resident_with_wide_contests(group
     sn = random_scalars(rng, (nb, man.nsel, 4), group.q)
     cn = random_scalars(rng, (nb, man.n_contests), group.q)
     eb = batch_encryption(group, key, 99, man, votes, sn, cn)
-    dev = torch.device("cuda", 0)
-    dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (votes, sn, cn))
-    oc = torch.empty(eb.cts.shape, dtype=torch.uint8, device=dev)
-    orp = torch.empty(eb.rproof.shape, dtype=torch.uint8, device=dev)
-    ocp = torch.empty(eb.cproof.shape, dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
-    batch_encryption_device(group, key, 99, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
-                            oc.data_ptr(), orp.data_ptr(), ocp.data_ptr())
-    assert np.array_equal(oc.cpu().numpy(), eb.cts)
-    assert np.array_equal(orp.cpu().numpy(), eb.rproof)
-    assert np.array_equal(ocp.cpu().numpy(), eb.cproof)
+    dv, dsn, dcn = (group.to_device(np.ascontiguousarray(x)) for x in (votes, sn, cn))
+    oc = group.device_empty(eb.cts.shape)
+    orp = group.device_empty(eb.rproof.shape)
+    ocp = group.device_empty(eb.cproof.shape)
+    batch_encryption_device(group, key, 99, man, nb, dv.ptr, dsn.ptr, dcn.ptr,
+                            oc.ptr, orp.ptr, ocp.ptr)
+    assert np.array_equal(oc.download(), eb.cts)
+    assert np.array_equal(orp.download(), eb.rproof)
+    assert np.array_equal(ocp.download(), eb.cproof)
 
 
 def test_wide_manifest_smaller_chunks(group):
@@ -285,7 +279,6 @@ def test_cast_mask_across_verify_chunks(group):
     host-pointer path (flags uploaded once, offset per chunk) and the device path: spoiled
     ballots on both sides of the boundary, the tally equals the CPython product over the cast
     ballots only; the verdicts of every ballot are still computed."""
-    import torch
     from electionguard.ballot import EncryptedBallots, Manifest, Verifier
     man = Manifest(1, 2, 1)
     nb = 16384 + 300
@@ -298,14 +291,12 @@ def test_cast_mask_across_verify_chunks(group):
     assert ok_s.all() and ok_c.all()
     want = _tally_products(man, EncryptedBallots(eb.cts[cast], eb.rproof[cast], eb.cproof[cast]))
     assert np.array_equal(tally, want)
-    dev = torch.device("cuda", 0)
-    d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (eb.cts, eb.rproof, eb.cproof)]
-    dm = torch.from_numpy(cast.astype(np.uint8)).to(dev)
-    oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
-    okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
-    tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
-    V.verify_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), nb, oks.data_ptr(), okc.data_ptr(),
-                    tal.data_ptr(), dm.data_ptr())
+    d = [group.to_device(np.ascontiguousarray(x)) for x in (eb.cts, eb.rproof, eb.cproof)]
+    dm = group.to_device(cast.astype(np.uint8))
+    oks = group.device_zeros((nb, man.nsel))
+    okc = group.device_zeros((nb, man.n_contests))
+    tal = group.device_zeros((man.n_real, 2, 512))
+    V.verify_device(d[0].ptr, d[1].ptr, d[2].ptr, nb, oks.ptr, okc.ptr,
+                    tal.ptr, dm.ptr)
     group.sync()
-    assert bool(oks.all()) and bool(okc.all()) and np.array_equal(tal.cpu().numpy(), want)
+    assert group.all_nonzero(oks) and group.all_nonzero(okc) and np.array_equal(tal.download(), want)

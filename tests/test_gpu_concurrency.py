@@ -104,12 +104,10 @@ def test_two_keys_on_one_context_device_paths(group):
     bytes against its own host encryption made before the threads start, and verifies on the
     device; a tally under the wrong key would fail the proofs."""
     import numpy as np
-    import torch
     from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption, batch_encryption_device,
                                       random_scalars, random_votes)
     from electionguard.keyceremony import key_ceremony
     man = Manifest(2, 3, 1)
-    dev = torch.device("cuda", 0)
     jobs = []
     for seed in (101, 202, 303):
         _, K = key_ceremony(group, 2, 2, seed=seed)
@@ -121,26 +119,24 @@ def test_two_keys_on_one_context_device_paths(group):
         cn = random_scalars(rng, (nb, man.n_contests), group.q)
         ref = batch_encryption(group, key, seed, man, votes, sn, cn)
         jobs.append((seed, key, nb, votes, sn, cn, ref))
-    torch.cuda.synchronize()
     ok = {}
 
     def run(seed, key, nb, votes, sn, cn, ref):
         def f():
-            dv, dsn, dcn = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (votes, sn, cn))
-            oc = torch.empty(ref.cts.shape, dtype=torch.uint8, device=dev)
-            orp = torch.empty(ref.rproof.shape, dtype=torch.uint8, device=dev)
-            ocp = torch.empty(ref.cproof.shape, dtype=torch.uint8, device=dev)
-            oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
-            okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
-            torch.cuda.synchronize()
+            dv, dsn, dcn = (group.to_device(np.ascontiguousarray(x)) for x in (votes, sn, cn))
+            oc = group.device_empty(ref.cts.shape)
+            orp = group.device_empty(ref.rproof.shape)
+            ocp = group.device_empty(ref.cproof.shape)
+            oks = group.device_zeros((nb, man.nsel))
+            okc = group.device_zeros((nb, man.n_contests))
             V = Verifier(group, key, seed, man)
             res = []
             for _ in range(4):
-                batch_encryption_device(group, key, seed, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
-                                        oc.data_ptr(), orp.data_ptr(), ocp.data_ptr())
-                V.verify_device(oc.data_ptr(), orp.data_ptr(), ocp.data_ptr(), nb, oks.data_ptr(), okc.data_ptr(), None)
+                batch_encryption_device(group, key, seed, man, nb, dv.ptr, dsn.ptr, dcn.ptr,
+                                        oc.ptr, orp.ptr, ocp.ptr)
+                V.verify_device(oc.ptr, orp.ptr, ocp.ptr, nb, oks.ptr, okc.ptr, None)
                 group.sync()
-                res.append(bool(np.array_equal(oc.cpu().numpy(), ref.cts)) and bool(oks.all()) and bool(okc.all()))
+                res.append(bool(np.array_equal(oc.download(), ref.cts)) and group.all_nonzero(oks) and group.all_nonzero(okc))
             ok[seed] = res
         return f
 

@@ -18,7 +18,6 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(group, contests, selections, nb, seed, trustees=False):
-    import torch
     from electionguard.ballot import (ElectionKey, Manifest, Verifier, batch_encryption_device, random_scalars,
                                       random_votes)
     from electionguard.decrypt import dlog_g_batch
@@ -29,32 +28,30 @@ def _run(group, contests, selections, nb, seed, trustees=False):
     key = ElectionKey(group, K, window_bits=16)
     rng = np.random.default_rng(seed)
     votes = random_votes(rng, man, nb)
-    dev = torch.device("cuda", 0)
-    dv = torch.from_numpy(votes).to(dev)
-    dsn = torch.from_numpy(random_scalars(rng, (nb, man.nsel, 4), group.q)).to(dev)
-    dcn = torch.from_numpy(random_scalars(rng, (nb, man.n_contests), group.q)).to(dev)
-    cts = torch.empty((nb, man.nsel, 2, 512), dtype=torch.uint8, device=dev)
-    rp = torch.empty((nb, man.nsel, 4, 32), dtype=torch.uint8, device=dev)
-    cp = torch.empty((nb, man.n_contests, 2, 32), dtype=torch.uint8, device=dev)
+    dv = group.to_device(votes)
+    dsn = group.to_device(random_scalars(rng, (nb, man.nsel, 4), group.q))
+    dcn = group.to_device(random_scalars(rng, (nb, man.n_contests), group.q))
+    cts = group.device_empty((nb, man.nsel, 2, 512))
+    rp = group.device_empty((nb, man.nsel, 4, 32))
+    cp = group.device_empty((nb, man.n_contests, 2, 32))
     qbar = 0xC0FFEE + seed
-    torch.cuda.synchronize()
-    batch_encryption_device(group, key, qbar, man, nb, dv.data_ptr(), dsn.data_ptr(), dcn.data_ptr(),
-                            cts.data_ptr(), rp.data_ptr(), cp.data_ptr())
+    batch_encryption_device(group, key, qbar, man, nb, dv.ptr, dsn.ptr, dcn.ptr,
+                            cts.ptr, rp.ptr, cp.ptr)
     del dsn, dcn
     V = Verifier(group, key, qbar, man)
 
     def verify(a, b):
-        oks = torch.zeros((b - a, man.nsel), dtype=torch.uint8, device=dev)
-        okc = torch.zeros((b - a, man.n_contests), dtype=torch.uint8, device=dev)
-        tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-        V.verify_device(cts[a:b].data_ptr(), rp[a:b].data_ptr(), cp[a:b].data_ptr(), b - a, oks.data_ptr(),
-                        okc.data_ptr(), tal.data_ptr())
+        oks = group.device_zeros((b - a, man.nsel))
+        okc = group.device_zeros((b - a, man.n_contests))
+        tal = group.device_zeros((man.n_real, 2, 512))
+        V.verify_device(cts[a:b].ptr, rp[a:b].ptr, cp[a:b].ptr, b - a, oks.ptr,
+                        okc.ptr, tal.ptr)
         group.sync()
-        return bool(oks.all().item() and okc.all().item()), tal
+        return group.all_nonzero(oks) and group.all_nonzero(okc), tal
 
     ok, tally = verify(0, nb)
     assert ok, "honest ballots rejected"
-    T = tally.cpu().numpy()
+    T = tally.download()
     want = votes.reshape(nb, man.n_contests, man.spc)[:, :, :man.n_selections].sum(axis=0).reshape(-1)
     if trustees:  # the trustees' shares: 3 of 5 guardians available, 2 compensated
         from electionguard.decrypt import DecryptingTrustee, Decryption
@@ -79,11 +76,14 @@ def _run(group, contests, selections, nb, seed, trustees=False):
         def is_initialized():
             return False
 
-    parts = np.stack([t_a.cpu().numpy(), t_b.cpu().numpy()])          # (world, n_real, 2, 512)
+    parts = np.stack([t_a.download(), t_b.download()])          # (world, n_real, 2, 512)
     g = np.ascontiguousarray(np.transpose(parts, (1, 2, 0, 3))).reshape(-1, 512)
     folded = group.prodP_groups(g, man.n_real * 2, 2).reshape(man.n_real, 2, 512)
     assert np.array_equal(folded, T)
-    assert gather_fold_tally(TwoRanks, tally, group.prodP_groups).tobytes() == T.tobytes()  # world 1: identity
+    assert gather_fold_tally(TwoRanks, T, group.prodP_groups).tobytes() == T.tobytes()  # world 1: identity
+    # the same fold in libeg_hip (eg_tally_allgather_fold without a communicator: the local parts)
+    d2 = group.to_device(parts)
+    assert np.array_equal(group.tally_allgather_fold(d2, 2, man.n_real * 2).reshape(man.n_real, 2, 512), T)
 
 
 def test_config2_one_rank_shard_125k(group):

@@ -105,10 +105,9 @@ def test_generic_odd_modulus(oracle_group):
 
 
 def test_powp_and_fb_dev_pointers(group, oracle_group):
-    """eg_powp_batch_dev / eg_fb_pow_batch_dev (operands resident in HBM, torch tensors'
+    """eg_powp_batch_dev / eg_fb_pow_batch_dev (operands resident in HBM, libeg_hip device buffers'
     data_ptr()): same results as the host-pointer calls and the oracle, incl. edge cases,
     a ragged size and a second call that reuses the cached job table."""
-    import torch
     O = oracle_group
     rng = random.Random(23)
     p, q = O.p, O.q
@@ -117,24 +116,24 @@ def test_powp_and_fb_dev_pointers(group, oracle_group):
     n = len(bases)
     B = np.stack([np.frombuffer(b.to_bytes(512, "big"), np.uint8) for b in bases])
     E = np.stack([np.frombuffer(e.to_bytes(32, "big"), np.uint8) for e in exps])
-    dB, dE = torch.from_numpy(B).cuda(), torch.from_numpy(E).cuda()
-    dO = torch.zeros((n, 512), dtype=torch.uint8, device="cuda")
+    dB, dE = group.to_device(B), group.to_device(E)
+    dO = group.device_zeros((n, 512))
     for _ in range(2):
-        dO.zero_()
-        group.powP_batch_dev(dB.data_ptr(), dE.data_ptr(), dO.data_ptr(), n)
+        dO.zero()
+        group.powP_batch_dev(dB.ptr, dE.ptr, dO.ptr, n)
         group.sync()
-        out = dO.cpu().numpy()
+        out = dO.download()
         for i in range(n):
             assert be2i(out[i]) == O.powP(bases[i], exps[i]), i
-    group.gPowP_batch_dev(dE.data_ptr(), dO.data_ptr(), n)
+    group.gPowP_batch_dev(dE.ptr, dO.ptr, n)
     group.sync()
-    out = dO.cpu().numpy()
+    out = dO.download()
     for i in range(n):
         assert be2i(out[i]) == O.gPowP(exps[i]), i
     fb = group.fixed_base(bases[20], window_bits=9)
-    fb.pow_batch_dev(dE.data_ptr(), dO.data_ptr(), 33)
+    fb.pow_batch_dev(dE.ptr, dO.ptr, 33)
     group.sync()
-    out = dO.cpu().numpy()
+    out = dO.download()
     for i in range(33):
         assert be2i(out[i]) == O.powP(bases[20], exps[i]), i
     fb.close()

@@ -88,7 +88,6 @@ def test_golden_cast_mask_and_spoiled_shares(case):
 
 
 def test_mixed_batch_cast_tally_and_spoiled_decryption(group):
-    import torch
     from electionguard.ballot import (ElectionKey, EncryptedBallots, Manifest, Verifier, accumulate_tally,
                                       batch_encryption, random_scalars, random_votes)
     from electionguard.decrypt import DecryptingTrustee, Decryption, verify_decryption_record
@@ -116,17 +115,15 @@ def test_mixed_batch_cast_tally_and_spoiled_decryption(group):
     assert np.array_equal(tally, want)
     assert np.array_equal(accumulate_tally(group, man, eb, cast), want)
     # device path with a device mask: same verdicts and tally
-    dev = torch.device("cuda", 0)
-    d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (eb.cts, eb.rproof, eb.cproof)]
-    dmask = torch.from_numpy(cast.astype(np.uint8)).to(dev)
-    oks = torch.zeros((nb, man.nsel), dtype=torch.uint8, device=dev)
-    okc = torch.zeros((nb, man.n_contests), dtype=torch.uint8, device=dev)
-    tal = torch.zeros((man.n_real, 2, 512), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
-    V.verify_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), nb, oks.data_ptr(), okc.data_ptr(),
-                    tal.data_ptr(), dmask.data_ptr())
+    d = [group.to_device(np.ascontiguousarray(x)) for x in (eb.cts, eb.rproof, eb.cproof)]
+    dmask = group.to_device(cast.astype(np.uint8))
+    oks = group.device_zeros((nb, man.nsel))
+    okc = group.device_zeros((nb, man.n_contests))
+    tal = group.device_zeros((man.n_real, 2, 512))
+    V.verify_device(d[0].ptr, d[1].ptr, d[2].ptr, nb, oks.ptr, okc.ptr,
+                    tal.ptr, dmask.ptr)
     group.sync()
-    assert bool(oks.all()) and bool(okc.all()) and np.array_equal(tal.cpu().numpy(), want)
+    assert group.all_nonzero(oks) and group.all_nonzero(okc) and np.array_equal(tal.download(), want)
     # the tally decrypts to the cast votes; the spoiled ballots to their own votes
     comm = {g.gid: g.commitments for g in gk}
     avail = [DecryptingTrustee(group, g, comm) for g in gk[:3]]

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 GPU checks on one MI355X (gpurun): the GPU suite, the default bench line and the 2-rank
+# gloo rehearsal of bench.py's N > 1 path (cpu_baseline + vs_baseline on rank 0's line).
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- 'bash tools/gpu_r04.sh r04a'
+set -eo pipefail
+TAG=${1:-r04a}
+STEPS=${STEPS:-tests,bench,gloo2}
+mkdir -p gpurun_out
+if [[ $STEPS == *tests* ]]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/${TAG}_gpu_tests.log 2>&1
+  echo "tests: $(tail -n 1 gpurun_out/${TAG}_gpu_tests.log)"
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
+  echo "bench: $(tail -c 300 gpurun_out/${TAG}_bench.log)"
+fi
+if [[ $STEPS == *gloo2* ]]; then
+  timeout -k 10 300 env EG_DIST_BACKEND=gloo python bench.py --gpus 2 --ballots 20000 --steps 2 --warmup 1 \
+    --modexp-n 4096 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo2.log 2>&1
+  echo "gloo2: $(tail -c 300 gpurun_out/${TAG}_rehearse_gloo2.log)"
+fi
+echo all done
