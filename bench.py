@@ -390,7 +390,7 @@ def encrypt_device_rate(group, key, qbar, man, votes, sn, cn, d_cts, d_rp, d_cp,
         run()
         dt = time.perf_counter() - t
         best = dt if best is None else min(best, dt)
-    same = all(np.array_equal(x.download(), y.download()) for x, y in ((oc, d_cts), (orp, d_rp), (ocp, d_cp)))
+    same = all(np.array_equal(x.download().ravel(), y.download().ravel()) for x, y in ((oc, d_cts), (orp, d_rp), (ocp, d_cp)))
     for b in (dv, dsn, dcn, oc, orp, ocp):
         b.free()
     if not same:
