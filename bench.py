@@ -520,8 +520,208 @@ def cpu_baseline(a, man, eb, qbar, K):
     }
 
 
-def full_pipeline(a, world, rank, local, dist):
-    raise SystemExit("--pipeline full: not built yet")
+def full_pipeline(a, world, rank, local, dist, keep=None):
+    """configs[4]'s full pipeline (RunRemoteWorkflowTest.java:140-182), ONE step per rank =
+      1 encrypt the rank's ballots on the device (batchEncryption :140-141; eg_encrypt_ballots_dev:
+        votes and injected nonces resident in HBM, ciphertexts and proofs written in HBM);
+      2 verify every proof + tally (Verifier :179-182, runAccumulateBallots :151;
+        eg_verify_ballots_dev on the ciphertexts step 1 wrote);
+      3 the verdict all-reduce and the partial-tally all-gather + mod-p fold (SURVEY §8e);
+      4 on rank 0: decryption of the folded tally through the DecryptingTrustees (the remote
+        decryption :164-172: each available guardian's direct shares, every (missing, available)
+        pair's compensated shares with recovery keys, every share proof checked, Lagrange combine,
+        BSGS dLog) -> counts, which must equal the vote totals over every rank exactly.
+    value = ballots through the whole pipeline per second over the node.  Per-phase times are
+    summed over the timed steps (max over ranks for phases 1-3).  keep (tests): a dict that
+    receives the step's artifacts."""
+    from electionguard.ballot import Verifier, batch_encryption_device
+    from electionguard.core import productionGroup
+    from electionguard.decrypt import DecryptingTrustee, Decryption
+    from electionguard.distributed import TallyExchange, max_over_ranks
+
+    if not 1 <= a.quorum <= a.available <= a.guardians:
+        raise SystemExit("--pipeline full needs quorum <= available <= guardians")
+    group = productionGroup(local)
+    man, gk, K, key, qbar, votes, sn, cn = setup_election(a, group, rank)
+    nb = a.ballots
+    want = votes.reshape(nb, man.n_contests, man.spc)[:, :, :man.n_selections].sum(axis=0).reshape(-1).astype(np.int64)
+    if dist is not None:  # the expected counts: the vote totals over every rank's shard
+        import torch
+        tw = torch.from_numpy(want.copy())
+        dist.all_reduce(tw)
+        want = tw.numpy()
+    dv, dsn, dcn = (group.to_device(x) for x in (votes, sn, cn))
+    d_cts = group.device_empty((nb, man.nsel, 2, 512))
+    d_rp = group.device_empty((nb, man.nsel, 4, 32))
+    d_cp = group.device_empty((nb, man.n_contests, 2, 32))
+    d_oks = group.device_buffer(nb * man.nsel)
+    d_okc = group.device_buffer(nb * man.n_contests)
+    d_tal = group.device_buffer(man.n_real * 2 * 512)
+    ver = Verifier(group, key, qbar, man)
+    dec = None
+    if rank == 0:
+        comm = {g.gid: g.commitments for g in gk}
+        dec = Decryption(group, qbar, [DecryptingTrustee(group, g, comm) for g in gk[:a.available]],
+                         [g.gid for g in gk[a.available:]], {g.gid: g.public_key for g in gk})
+    xch = TallyExchange(group, dist, world, rank, exchange_mode())
+    ph = {"encrypt": 0.0, "verify_tally": 0.0, "exchange": 0.0, "decrypt": 0.0}
+    counts = None
+    last = {}
+
+    def step(acc):
+        nonlocal counts
+        t0 = time.perf_counter()
+        batch_encryption_device(group, key, qbar, man, nb, dv.ptr, dsn.ptr, dcn.ptr, d_cts.ptr, d_rp.ptr, d_cp.ptr)
+        t1 = time.perf_counter()  # (returns when the outputs are written)
+        ver.verify_device(d_cts.ptr, d_rp.ptr, d_cp.ptr, nb, d_oks.ptr, d_okc.ptr, d_tal.ptr)
+        ok = group.all_nonzero(d_oks) and group.all_nonzero(d_okc)  # (synchronises the stream)
+        t2 = time.perf_counter()
+        ok = xch.all_valid(ok)
+        T = xch.fold(d_tal, man.n_real)
+        t3 = time.perf_counter()
+        if not ok:
+            raise RuntimeError("verification failed on honest synthetic ballots")
+        if rank == 0:
+            last["tally"] = T
+            counts = dec.decrypt(T, nb * world)
+            if [int(x) if x is not None else None for x in counts] != [int(x) for x in want]:
+                raise RuntimeError("decrypted counts differ from the vote totals")
+            if keep is not None:
+                keep["tally"], keep["counts"] = T, counts
+        t4 = time.perf_counter()
+        if acc:
+            ph["encrypt"] += t1 - t0
+            ph["verify_tally"] += t2 - t1
+            ph["exchange"] += t3 - t2
+            ph["decrypt"] += t4 - t3
+
+    for _ in range(a.warmup):
+        step(False)
+    if dist:
+        dist.barrier()
+    group.sync()
+    group.profile_begin()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    group.sync()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kp = group.profile_end()
+    el = max_over_ranks(dist, el)
+    phases = {k: max_over_ranks(dist, v) for k, v in ph.items()}
+    xch.close()
+    value = nb * world * a.steps / el
+    out = line_common(a, world, el, value, kp, nb, man,
+                      "ballots encrypted+verified+tallied+decrypted/sec (node, 4096-bit group, full pipeline)",
+                      xch.collective)
+    tot = nb * world * a.steps
+    out["phases"] = {
+        "encrypt": {"s": round(phases["encrypt"], 3), "ballots_per_s": round(tot / phases["encrypt"], 1)},
+        "verify_tally": {"s": round(phases["verify_tally"], 3),
+                         "ballots_per_s": round(tot / phases["verify_tally"], 1)},
+        "exchange": {"s": round(phases["exchange"], 4)},
+        "decrypt": {"s": round(phases["decrypt"], 3), "texts": man.n_real,
+                    "trustees": f"{a.available} of {a.guardians} available, quorum {a.quorum}, "
+                                f"{a.guardians - a.available} missing (direct + compensated shares with proofs)",
+                    "note": "rank 0 only; the other ranks wait at the next exchange"},
+        "counts_exact": True,
+    }
+    sample = None
+    if rank == 0 and a.cpu_sample > 0:
+        ns = min(nb, a.cpu_max_ballots)
+        sample = (votes[:ns], sn[:ns], cn[:ns], d_cts[0:ns].download(), d_rp[0:ns].download(), d_cp[0:ns].download())
+    if keep is not None:
+        keep["group"], keep["K"], keep["qbar"], keep["man"], keep["gk"] = group, K, qbar, man, gk
+        keep["want"], keep["cts"], keep["rproof"], keep["cproof"] = want, d_cts.download(), d_rp.download(), d_cp.download()
+    if world > 1:
+        dist.barrier()
+    if sample is not None:
+        out["cpu_baseline"] = cpu_baseline_pipeline(a, man, sample, qbar, K, gk, nb * world, phases, last["tally"])
+        attach_ratio(out)
+    return out
+
+
+def cpu_baseline_pipeline(a, man, sample, qbar, K, gk, nb_total, gpu_phases, tally):
+    """The CPU port (oracle/eg_oracle_c.c: OpenSSL BN, 8-bit radix fixed base) on the pipeline's
+    phases, on the lease's cores: batchEncryption and verify + tally on a calibrated sample of the
+    same ballots (the encryption must reproduce the GPU's bytes), and the trustees' direct +
+    compensated shares of one tally (the mediator's share-proof checks and the dLog are not timed on
+    the CPU: a lower bound for its decrypt phase).  value = the node's ballots per CPU step time
+    projected from the per-phase rates: nb_total / (nb_total / encrypt + nb_total / verify + decrypt)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from eg_oracle_c import COracle
+    from electionguard.core import constants as C
+    from electionguard.keyceremony import poly_eval
+
+    votes, sn, cn, cts, rp, cp = sample
+    threads, affinity, quota_cpus = cpu_threads(a)
+    co = COracle(C.P, C.Q, C.G)
+    co.set_key(K)
+    per = a.cpu_seconds / 3
+
+    def enc(n):
+        t = time.perf_counter()
+        c2, r2, p2 = co.encrypt_ballots(qbar, man.n_contests, man.spc, votes[:n], sn[:n], cn[:n], threads=threads)
+        dt = time.perf_counter() - t
+        if not (np.array_equal(c2, cts[:n]) and np.array_equal(r2, rp[:n]) and np.array_equal(p2, cp[:n])):
+            raise RuntimeError("the CPU port's encryption differs from the GPU's bytes")
+        return dt
+
+    def ver(n):
+        t = time.perf_counter()
+        ok_s, ok_c, _ = co.verify_ballots(qbar, man.n_contests, man.spc, 1, 1, cts[:n], rp[:n], cp[:n], threads=threads)
+        dt = time.perf_counter() - t
+        if not (ok_s.all() and ok_c.all()):
+            raise RuntimeError("the CPU port rejects the GPU's ballots")
+        return dt
+
+    n_all = len(votes)
+    rates = {}
+    for name, fn in (("encrypt", enc), ("verify_tally", ver)):
+        n0 = min(n_all, 2 * threads)
+        dt0 = fn(n0)
+        s = max(n0, min(n_all, int(n0 / dt0 * per)))
+        rates[name] = (s, s / fn(s))
+    # the decrypt phase: every share of one tally (n_real texts) on the CPU
+    rng = np.random.default_rng(5)
+    texts = np.ascontiguousarray(tally, np.uint8).reshape(man.n_real, 2, 512)
+    nonces = rng.integers(0, 256, size=(man.n_real, 32), dtype=np.uint8)
+    avail, missing = gk[:a.available], gk[a.available:]
+    t = time.perf_counter()
+    for g in avail:
+        co.trustee_decrypt(g.secret, qbar, texts, nonces, threads=threads)
+    for l in missing:
+        for g in avail:
+            co.trustee_decrypt(poly_eval(l.coeffs, g.x, C.Q), qbar, texts, nonces, threads=threads)
+    t_dec = time.perf_counter() - t
+    enc_rate, ver_rate = rates["encrypt"][1], rates["verify_tally"][1]
+    value = nb_total / (nb_total / enc_rate + nb_total / ver_rate + t_dec)
+    quota = f", cgroup CPU quota {quota_cpus:.1f}" if quota_cpus else ", no cgroup CPU quota"
+    model = cpu_model()
+    nshares = man.n_real * len(avail) * (1 + len(missing))
+    return {
+        "value": round(value, 3),
+        "unit": "ballots/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"encrypt {rates['encrypt'][0]} and verify + tally {rates['verify_tally'][0]} of the same ballots "
+                  f"(the CPU encryption reproduced the GPU's bytes; every verdict valid), and the {nshares} trustee "
+                  f"shares of one {man.n_real}-text tally (share checks and dLog not timed on the CPU); projected to "
+                  f"{nb_total} ballots per step; {threads} threads = the lease's usable CPUs (affinity {affinity} of "
+                  f"{os.cpu_count()}{quota}) on {model or 'host CPU'}; OpenSSL BN_mod_exp_mont + 8-bit radix fixed base",
+        "phases": {"encrypt_ballots_per_s": round(enc_rate, 3), "verify_tally_ballots_per_s": round(ver_rate, 3),
+                   "decrypt_shares_s": round(t_dec, 3)},
+        "gpu_over_cpu_by_phase": {
+            "encrypt": round(nb_total * a.steps / gpu_phases["encrypt"] / enc_rate, 1) if gpu_phases["encrypt"] else None,
+            "verify_tally": round(nb_total * a.steps / gpu_phases["verify_tally"] / ver_rate, 1)
+            if gpu_phases["verify_tally"] else None,
+        },
+        "cpu_model": model,
+        "affinity_cpus": affinity,
+        "cgroup_quota_cpus": quota_cpus,
+    }
 
 
 if __name__ == "__main__":

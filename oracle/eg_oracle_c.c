@@ -307,3 +307,176 @@ int ego_gpowp(const uint8_t* exp, uint8_t* out, size_t n) {
   BN_CTX_free(ctx);
   return 0;
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * Encryption with injected nonces (batchEncryption, RunRemoteWorkflowTest.java:140-141), restating
+ * eg_oracle.py:encrypt / make_range_proof / make_constant_proof.  Per selection (R, u, c_fake,
+ * v_fake): alpha = g^R, beta = K^R g^m; the real branch commits (g^u, K^u), the fake branch is
+ * simulated with the known nonce: a_f = g^(v_f + R c_f), b_f = K^(v_f + R c_f) g^(+-c_f) (the
+ * values of g^v_f alpha^c_f and K^v_f (beta g^-f)^c_f); c = H(qbar, alpha, beta, a0, b0, a1, b1),
+ * c_real = c - c_f, v_real = u - c_real R.  Per contest: (g^u, K^u), c = H(qbar, A, B, a, b),
+ * v = u - c R_sum.  Fixed-base terms use the 8-bit radix tables (LOW_MEMORY_USE).
+ * --------------------------------------------------------------------------------------------- */
+typedef struct {
+  size_t b0, b1, nc, spc;
+  const uint8_t *qbar, *votes, *sn, *cn;
+  uint8_t *cts, *rproof, *cproof;
+} EncJob;
+
+static void q_bytes(uint8_t out[32], const BIGNUM* x) { BN_bn2binpad(x, out, 32); }
+
+static void* encrypt_worker(void* arg) {
+  EncJob* J = (EncJob*)arg;
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM *qbar = bn_be(J->qbar, 32), *al = BN_new(), *be = BN_new(), *t1 = BN_new(), *t2 = BN_new();
+  BIGNUM *ar = BN_new(), *br = BN_new(), *af = BN_new(), *bf = BN_new(), *h = BN_new();
+  BIGNUM *R = BN_new(), *u = BN_new(), *cf = BN_new(), *vf = BN_new(), *sf = BN_new(), *cr = BN_new(), *vr = BN_new();
+  BIGNUM *A = BN_new(), *B = BN_new(), *Rs = BN_new();
+  BIGNUM* el[6];
+  uint8_t e[32];
+  const size_t nsel = J->nc * J->spc;
+  for (size_t b = J->b0; b < J->b1; ++b) {
+    for (size_t k = 0; k < J->nc; ++k) {
+      BN_one(A);
+      BN_one(B);
+      BN_zero(Rs);
+      for (size_t s = 0; s < J->spc; ++s) {
+        const size_t i = b * nsel + k * J->spc + s;
+        const uint8_t* n4 = J->sn + i * 128;
+        const int m = J->votes[i] != 0;
+        BN_bin2bn(n4, 32, R);
+        BN_bin2bn(n4 + 32, 32, u);
+        BN_bin2bn(n4 + 64, 32, cf);
+        BN_bin2bn(n4 + 96, 32, vf);
+        radix_pow(al, RG, n4, ctx);                 /* alpha = g^R */
+        radix_pow(be, RK, n4, ctx);                 /* beta = K^R g^m */
+        if (m) mulp(be, be, G.g, ctx);
+        radix_pow(ar, RG, n4 + 32, ctx);            /* real branch: g^u, K^u */
+        radix_pow(br, RK, n4 + 32, ctx);
+        BN_mod_mul(sf, R, cf, G.q, ctx);            /* s_f = v_f + R c_f */
+        BN_mod_add(sf, sf, vf, G.q, ctx);
+        q_bytes(e, sf);
+        radix_pow(af, RG, e, ctx);
+        radix_pow(bf, RK, e, ctx);
+        if (m) BN_copy(t1, cf);                     /* g^(c_f) for m = 1, g^(-c_f) for m = 0 */
+        else {
+          BN_sub(t1, G.q, cf);
+          BN_nnmod(t1, t1, G.q, ctx);
+        }
+        q_bytes(e, t1);
+        radix_pow(t2, RG, e, ctx);
+        mulp(bf, bf, t2, ctx);
+        el[0] = al; el[1] = be;
+        if (m == 0) { el[2] = ar; el[3] = br; el[4] = af; el[5] = bf; }
+        else { el[2] = af; el[3] = bf; el[4] = ar; el[5] = br; }
+        hash_elems(h, qbar, el, 6, ctx);
+        BN_mod_sub(cr, h, cf, G.q, ctx);            /* c_real = c - c_f */
+        BN_mod_mul(t1, cr, R, G.q, ctx);            /* v_real = u - c_real R */
+        BN_mod_sub(vr, u, t1, G.q, ctx);
+        uint8_t* ct = J->cts + i * 1024;
+        BN_bn2binpad(al, ct, 512);
+        BN_bn2binpad(be, ct + 512, 512);
+        uint8_t* pr = J->rproof + i * 128;
+        if (m == 0) { q_bytes(pr, cr); q_bytes(pr + 32, vr); q_bytes(pr + 64, cf); q_bytes(pr + 96, vf); }
+        else { q_bytes(pr, cf); q_bytes(pr + 32, vf); q_bytes(pr + 64, cr); q_bytes(pr + 96, vr); }
+        mulp(A, A, al, ctx);
+        mulp(B, B, be, ctx);
+        BN_mod_add(Rs, Rs, R, G.q, ctx);
+      }
+      const uint8_t* uc = J->cn + (b * J->nc + k) * 32;
+      BN_bin2bn(uc, 32, u);
+      radix_pow(ar, RG, uc, ctx);
+      radix_pow(br, RK, uc, ctx);
+      el[0] = A; el[1] = B; el[2] = ar; el[3] = br;
+      hash_elems(h, qbar, el, 4, ctx);
+      BN_mod_mul(t1, h, Rs, G.q, ctx);              /* v = u - c R_sum */
+      BN_mod_sub(vr, u, t1, G.q, ctx);
+      uint8_t* cp = J->cproof + (b * J->nc + k) * 64;
+      q_bytes(cp, h);
+      q_bytes(cp + 32, vr);
+    }
+  }
+  BIGNUM* all[] = {qbar, al, be, t1, t2, ar, br, af, bf, h, R, u, cf, vf, sf, cr, vr, A, B, Rs};
+  for (size_t i = 0; i < sizeof(all) / sizeof(all[0]); ++i) BN_free(all[i]);
+  BN_CTX_free(ctx);
+  return NULL;
+}
+
+/* Encrypt nb ballots (layouts as include/eg_hip.h eg_encrypt_ballots). */
+int ego_encrypt_ballots(const uint8_t qbar[32], size_t nb, size_t nc, size_t spc, const uint8_t* votes,
+                        const uint8_t* sel_nonces, const uint8_t* contest_nonces, uint8_t* cts, uint8_t* rproof,
+                        uint8_t* cproof, int threads) {
+  if (!RK) return 1;
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  EncJob* jobs = (EncJob*)calloc(threads, sizeof(EncJob));
+  for (int t = 0; t < threads; ++t) {
+    EncJob* J = &jobs[t];
+    J->b0 = nb * t / threads;
+    J->b1 = nb * (t + 1) / threads;
+    J->nc = nc; J->spc = spc; J->qbar = qbar; J->votes = votes; J->sn = sel_nonces; J->cn = contest_nonces;
+    J->cts = cts; J->rproof = rproof; J->cproof = cproof;
+    pthread_create(&th[t], NULL, encrypt_worker, J);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Trustee partial decryption (DecryptingTrusteeIF.directDecrypt / compensatedDecrypt,
+ * RunRemoteDecryptingTrustee.java:189-193,227-232), restating eg_oracle.py:direct_decrypt: per
+ * text, M = pad^s, proof nonce u: a = g^u, b = pad^u, c = H(qbar, pad, data, a, b, M), v = u - c s.
+ * --------------------------------------------------------------------------------------------- */
+typedef struct {
+  size_t i0, i1;
+  const uint8_t *secret, *qbar, *texts, *nonces;
+  uint8_t *M, *proof;
+} TrJob;
+
+static void* trustee_worker(void* arg) {
+  TrJob* J = (TrJob*)arg;
+  BN_CTX* ctx = BN_CTX_new();
+  BIGNUM *qbar = bn_be(J->qbar, 32), *s = bn_be(J->secret, 32), *pad = BN_new(), *dat = BN_new(), *M = BN_new();
+  BIGNUM *u = BN_new(), *a = BN_new(), *b = BN_new(), *h = BN_new(), *t = BN_new(), *v = BN_new();
+  BIGNUM* el[5];
+  for (size_t i = J->i0; i < J->i1; ++i) {
+    BN_bin2bn(J->texts + i * 1024, 512, pad);
+    BN_bin2bn(J->texts + i * 1024 + 512, 512, dat);
+    BN_bin2bn(J->nonces + i * 32, 32, u);
+    BN_mod_exp_mont(M, pad, s, G.p, ctx, G.mont);
+    radix_pow(a, RG, J->nonces + i * 32, ctx);
+    BN_mod_exp_mont(b, pad, u, G.p, ctx, G.mont);
+    el[0] = pad; el[1] = dat; el[2] = a; el[3] = b; el[4] = M;
+    hash_elems(h, qbar, el, 5, ctx);
+    BN_mod_mul(t, h, s, G.q, ctx);
+    BN_mod_sub(v, u, t, G.q, ctx);
+    BN_bn2binpad(M, J->M + i * 512, 512);
+    q_bytes(J->proof + i * 64, h);
+    q_bytes(J->proof + i * 64 + 32, v);
+  }
+  BIGNUM* all[] = {qbar, s, pad, dat, M, u, a, b, h, t, v};
+  for (size_t i = 0; i < sizeof(all) / sizeof(all[0]); ++i) BN_free(all[i]);
+  BN_CTX_free(ctx);
+  return NULL;
+}
+
+int ego_trustee_decrypt(const uint8_t secret[32], const uint8_t qbar[32], const uint8_t* texts, const uint8_t* nonces,
+                        size_t n, uint8_t* out_M, uint8_t* out_proof, int threads) {
+  if (!RG) RG = radix_build(G.g);
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  TrJob* jobs = (TrJob*)calloc(threads, sizeof(TrJob));
+  for (int t = 0; t < threads; ++t) {
+    TrJob* J = &jobs[t];
+    J->i0 = n * t / threads;
+    J->i1 = n * (t + 1) / threads;
+    J->secret = secret; J->qbar = qbar; J->texts = texts; J->nonces = nonces; J->M = out_M; J->proof = out_proof;
+    pthread_create(&th[t], NULL, trustee_worker, J);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
+}

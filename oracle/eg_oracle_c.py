@@ -27,6 +27,8 @@ def load():
         _lib.ego_verify_ballots.argtypes = [P, S, S, S, S, ctypes.c_uint32, P, P, P, P, P, P, ctypes.c_int]
         _lib.ego_powp.argtypes = [P, P, P, S]
         _lib.ego_gpowp.argtypes = [P, P, S]
+        _lib.ego_encrypt_ballots.argtypes = [P, S, S, S, P, P, P, P, P, P, ctypes.c_int]
+        _lib.ego_trustee_decrypt.argtypes = [P, P, P, P, S, P, P, ctypes.c_int]
     return _lib
 
 
@@ -75,3 +77,30 @@ class COracle:
                                          _p(ok_s), _p(ok_c), _p(t), threads)
         assert rc == 0
         return ok_s.astype(bool), ok_c.astype(bool), t
+
+    def encrypt_ballots(self, qbar: int, nc: int, spc: int, votes, sel_nonces, contest_nonces, threads: int = 1):
+        """batchEncryption with injected nonces (eg_oracle.py:encrypt_ballot's algorithm, the
+        known-nonce fake branch); -> (cts, rproof, cproof) in the eg_encrypt_ballots layout."""
+        votes = np.ascontiguousarray(votes, np.uint8)
+        nb = votes.shape[0]
+        sn = np.ascontiguousarray(sel_nonces, np.uint8).reshape(nb, nc * spc, 4, 32)
+        cn = np.ascontiguousarray(contest_nonces, np.uint8).reshape(nb, nc, 32)
+        cts = np.zeros((nb, nc * spc, 2, 512), np.uint8)
+        rp = np.zeros((nb, nc * spc, 4, 32), np.uint8)
+        cp = np.zeros((nb, nc, 2, 32), np.uint8)
+        qb = _b(qbar, 32)
+        rc = self.lib.ego_encrypt_ballots(_p(qb), nb, nc, spc, _p(votes), _p(sn), _p(cn), _p(cts), _p(rp), _p(cp),
+                                          threads)
+        assert rc == 0, "set_key first"
+        return cts, rp, cp
+
+    def trustee_decrypt(self, secret: int, qbar: int, texts, nonces, threads: int = 1):
+        """directDecrypt (or compensatedDecrypt with secret = P_l(x_i)): -> (M (n, 512), proof (n, 2, 32))."""
+        texts = np.ascontiguousarray(texts, np.uint8).reshape(-1, 2, 512)
+        n = texts.shape[0]
+        nonces = np.ascontiguousarray(nonces, np.uint8).reshape(n, 32)
+        M = np.zeros((n, 512), np.uint8)
+        pr = np.zeros((n, 2, 32), np.uint8)
+        sb, qb = _b(secret, 32), _b(qbar, 32)
+        assert self.lib.ego_trustee_decrypt(_p(sb), _p(qb), _p(texts), _p(nonces), n, _p(M), _p(pr), threads) == 0
+        return M, pr

@@ -117,6 +117,41 @@ def test_c_oracle_verifies_golden_ballots_and_tally(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_c_oracle_encrypts_golden_ballots_byte_exact(mode):
+    """The C oracle's batchEncryption (known-nonce fake branch, 8-bit radix tables) reproduces the
+    golden ballots' bytes from their injected nonces: ciphertexts, range proofs and contest proofs."""
+    from eg_oracle_c import COracle
+    G = O.production_group(mode)
+    d, (nc, ns, va, spc), cts, rp, cp = golden_ballot_arrays(mode)
+    co = COracle(G.p, G.q, G.g)
+    co.set_key(h(d["K"]))
+    votes = np.array([b["votes"] for b in d["ballots"]], np.uint8)
+    sn = np.stack([_arr([x for n4 in b["nonces"] for x in n4], 32).reshape(-1, 4, 32) for b in d["ballots"]])
+    cn = np.stack([_arr(b["contest_nonces"], 32) for b in d["ballots"]])
+    for threads in (1, 2):
+        c2, r2, p2 = co.encrypt_ballots(h(d["qbar"]), nc, spc, votes, sn, cn, threads=threads)
+        assert np.array_equal(c2, cts) and np.array_equal(r2, rp) and np.array_equal(p2, cp)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c_oracle_trustee_golden(mode):
+    """The C oracle's directDecrypt / compensatedDecrypt reproduce the golden shares and proofs."""
+    from eg_oracle_c import COracle
+    G = O.production_group(mode)
+    d = load("trustee.json", mode)
+    co = COracle(G.p, G.q, G.g)
+    T = np.stack([_arr(t, 512) for t in d["texts"]])
+    N = _arr(d["nonces"], 32)
+    M, pr = co.trustee_decrypt(h(d["guardians"][0]["coeffs"][0]), h(d["qbar"]), T, N, threads=3)
+    assert [(m.tobytes().hex(), p[0].tobytes().hex(), p[1].tobytes().hex()) for m, p in zip(M, pr)] == \
+        [(w["M"], w["c"], w["v"]) for w in d["direct"]]
+    share = O.poly_eval([h(a) for a in d["guardians"][2]["coeffs"]], 2, O.Q)
+    M, pr = co.trustee_decrypt(share, h(d["qbar"]), T, N)
+    assert [(m.tobytes().hex(), p[0].tobytes().hex(), p[1].tobytes().hex()) for m, p in zip(M, pr)] == \
+        [(w["M"], w["c"], w["v"]) for w in d["compensated_by_x2_for_x3"]]
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_python_oracle_trustee_golden(mode):
     G = O.production_group(mode)
     d = load("trustee.json", mode)

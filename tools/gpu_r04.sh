@@ -20,4 +20,18 @@ if [[ $STEPS == *gloo2* ]]; then
     --modexp-n 4096 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo2.log 2>&1
   echo "gloo2: $(tail -c 300 gpurun_out/${TAG}_rehearse_gloo2.log)"
 fi
+if [[ $STEPS == *ptest* ]]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_comm.py -m gpu -x -v --timeout 300 \
+    --timeout-method thread > gpurun_out/${TAG}_gpu_tests_pipeline.log 2>&1
+  echo "ptest: $(tail -n 1 gpurun_out/${TAG}_gpu_tests_pipeline.log)"
+fi
+if [[ $STEPS == *pipe1* ]]; then
+  timeout -k 10 600 python bench.py --pipeline full > gpurun_out/${TAG}_bench_pipeline_config4.log 2>&1
+  echo "pipe1: $(tail -c 400 gpurun_out/${TAG}_bench_pipeline_config4.log)"
+fi
+if [[ $STEPS == *pipeg2* ]]; then
+  timeout -k 10 600 env EG_DIST_BACKEND=gloo python bench.py --gpus 2 --pipeline full --ballots 20000 --steps 1 \
+    --warmup 1 --modexp-n 0 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo2_pipeline.log 2>&1
+  echo "pipeg2: $(tail -c 400 gpurun_out/${TAG}_rehearse_gloo2_pipeline.log)"
+fi
 echo all done
