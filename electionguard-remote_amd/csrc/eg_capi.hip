@@ -150,7 +150,7 @@ constexpr int kCtEncWindow = 6;
 
 enum Slot {
   W_IN0, W_IN1, W_EXP, W_OUT, W_E0, W_E1, W_E2, W_E3, W_JOBS, W_SCR, W_TMP, W_FLAGS, W_SCAL,
-  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_CRF, W_CAST, W_ANY, W_GATHER, W_NSLOT
+  W_BE0, W_BE1, W_BE2, W_OK0, W_OK1, W_OFF, W_H0, W_H1, W_H2, W_H3, W_H4, W_H5, W_H6, W_H7, W_H8, W_EB0, W_EB1, W_EB2, W_EA2, W_YA, W_YB, W_RZ, W_CRF, W_CAST, W_ANY, W_GATHER, W_KBE, W_NSLOT
 };
 
 struct eg_ctx {
@@ -166,6 +166,8 @@ struct eg_ctx {
   eg_fixed_base* Ktab = nullptr;  // the current election key's radix table (keys.front().fb)
   uint32_t* d_gcomb = nullptr;  // Lim-Lee comb subset table of g (32 elements) for constant-time g^u
   uint32_t hash_fmt = EG_HASH_FIXED_WIDTH;  // Fiat-Shamir pre-image hex format (eg_ctx_set_hash_format)
+  uint32_t resp_plus = 0;  // response convention (eg_ctx_set_proof_format): 0 = v = u - c x, 1 = v = u + c x
+  uint32_t pre_order = EG_PREIMAGE_MESSAGE_FIRST;  // challenge pre-image element order
   DevBuf ws[W_NSLOT];
   bool timing = false;
   std::vector<ProfRec> prof;
@@ -180,6 +182,7 @@ struct eg_ctx {
     std::array<uint8_t, 512> K;
     eg_fixed_base* fb = nullptr;
     eg_fixed_base* ct = nullptr;
+    uint8_t* d_K = nullptr;  // K's 512 big-endian bytes in HBM (the EG_PREIMAGE_WITH_KEY hash element)
   };
   std::vector<KeyTabs> keys;
   std::map<std::string, DevBuf> cache;  // shape-keyed job tables
@@ -764,6 +767,7 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
   for (auto& k : c->keys) {
     eg_fixed_base_destroy(k.fb);
     eg_fixed_base_destroy(k.ct);
+    if (k.d_K) hipFree(k.d_K);
   }
   eg_fixed_base_destroy(c->g_ct);
   for (auto& kv : c->share_keys) eg_fixed_base_destroy(kv.second);
@@ -808,6 +812,17 @@ extern "C" int eg_ctx_set_hash_format(eg_ctx* c, int format) {
   if (format != EG_HASH_FIXED_WIDTH && format != EG_HASH_MINIMAL) return fail(EG_ERR_ARG, "unknown hash format");
   std::lock_guard<std::mutex> lk(c->mu);
   c->hash_fmt = (uint32_t)format;
+  return EG_OK;
+}
+
+extern "C" int eg_ctx_set_proof_format(eg_ctx* c, int response, int preimage) {
+  if (!c) return fail(EG_ERR_ARG, "null ctx");
+  if (response != EG_RESPONSE_MINUS && response != EG_RESPONSE_PLUS) return fail(EG_ERR_ARG, "unknown response convention");
+  if (preimage < EG_PREIMAGE_MESSAGE_FIRST || preimage > EG_PREIMAGE_WITH_KEY)
+    return fail(EG_ERR_ARG, "unknown pre-image order");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->resp_plus = response == EG_RESPONSE_PLUS ? 1u : 0u;
+  c->pre_order = (uint32_t)preimage;
   return EG_OK;
 }
 

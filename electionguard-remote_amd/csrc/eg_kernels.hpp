@@ -904,9 +904,12 @@ __device__ __noinline__ U256 mulmod256(const U256& a, const U256& b, const U256&
 
 // Encryption scalars, one thread per selection (nonces n = (R, u, c_fake, v_fake)):
 //   s_fake = v_fake + R*c_fake, s_gneg = m ? c_fake : -c_fake, mscal = m   (mod q)
-// (known-nonce simulation of the fake branch: a_f = g^s_fake, b_f = K^s_fake g^(+-c_fake))
+// (known-nonce simulation of the fake branch: a_f = g^s_fake, b_f = K^s_fake g^(+-c_fake)).
+// plus (eg_ctx_set_proof_format EG_RESPONSE_PLUS: a = g^v X^-c): s_fake = v_fake - R*c_fake and
+// s_gneg = m ? -c_fake : c_fake.  The response convention is public; the vote stays masked.
 __global__ void k_enc_prep(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ votes,
-                           const uint8_t* __restrict__ nonces, uint32_t n, uint8_t* __restrict__ derived) {
+                           const uint8_t* __restrict__ nonces, uint32_t n, uint8_t* __restrict__ derived,
+                           uint32_t plus) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const U256 q = ld256(q_be);
@@ -914,8 +917,10 @@ __global__ void k_enc_prep(const uint8_t* __restrict__ q_be, const uint8_t* __re
   const U256 cf = ld256(nonces + ((size_t)i * 4 + 2) * 32);
   const U256 vf = ld256(nonces + ((size_t)i * 4 + 3) * 32);
   const uint32_t m = votes[i] ? 1u : 0u;
-  const U256 sf = addmod256(vf, mulmod256(R, cf, q), q);
-  const U256 sg = sel256(0u - m, cf, negmod(cf, q));  // m ? c_fake : -c_fake, branch-free (secret vote)
+  const U256 Rc = mulmod256(R, cf, q);
+  const U256 sf = plus ? submod256(vf, Rc, q) : addmod256(vf, Rc, q);
+  // (m xor plus) ? c_fake : -c_fake, branch-free in the (secret) vote
+  const U256 sg = sel256((0u - m) ^ (0u - (plus & 1u)), cf, negmod(cf, q));
   U256 ms;
   for (int k = 0; k < 8; ++k) ms.w[k] = 0;
   ms.w[0] = m;
@@ -936,10 +941,10 @@ __global__ void k_enc_rsum(const uint8_t* __restrict__ q_be, const uint8_t* __re
   st256(rsum + (size_t)j * 32, r);
 }
 
-// Finish the range proofs: c_real = c - c_fake, v_real = u - c_real*R; arrange by m.
+// Finish the range proofs: c_real = c - c_fake, v_real = u - c_real*R (plus: u + c_real*R); arrange by m.
 __global__ void k_enc_finish(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ votes,
                              const uint8_t* __restrict__ nonces, const uint8_t* __restrict__ chal, uint32_t n,
-                             uint8_t* __restrict__ rproof) {
+                             uint8_t* __restrict__ rproof, uint32_t plus) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const U256 q = ld256(q_be);
@@ -949,7 +954,8 @@ __global__ void k_enc_finish(const uint8_t* __restrict__ q_be, const uint8_t* __
   const U256 vf = ld256(nonces + ((size_t)i * 4 + 3) * 32);
   const U256 c = ld256(chal + (size_t)i * 32);
   const U256 cr = submod256(c, cf, q);
-  const U256 vr = submod256(u, mulmod256(cr, R, q), q);
+  const U256 cR = mulmod256(cr, R, q);
+  const U256 vr = plus ? addmod256(u, cR, q) : submod256(u, cR, q);
   uint8_t* o = rproof + (size_t)i * 4 * 32;
   const uint32_t mk = 0u - (uint32_t)(votes[i] != 0);  // the branch order follows the vote: masked
   st256(o + 0, sel256(mk, cf, cr));
@@ -977,18 +983,19 @@ __global__ void k_enc_order(uint32_t* __restrict__ comm, const uint8_t* __restri
                    (b.w & ~mk) | (a.w & mk));
 }
 
-// Generic response v = u - c*x mod q (x per item or shared when x_stride == 0);
+// Generic response v = u - c*x mod q (plus: u + c*x; x per item or shared when x_stride == 0);
 // writes proof (c, v) as 2 x 32 B.
 __global__ void k_response(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ u_be,
                            const uint8_t* __restrict__ chal, const uint8_t* __restrict__ x_be, uint32_t x_stride,
-                           uint32_t n, uint8_t* __restrict__ proof) {
+                           uint32_t n, uint8_t* __restrict__ proof, uint32_t plus) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const U256 q = ld256(q_be);
   const U256 u = ld256(u_be + (size_t)i * 32);
   const U256 c = ld256(chal + (size_t)i * 32);
   const U256 x = ld256(x_be + (size_t)i * x_stride);
-  const U256 v = submod256(u, mulmod256(c, x, q), q);
+  const U256 cx = mulmod256(c, x, q);
+  const U256 v = plus ? addmod256(u, cx, q) : submod256(u, cx, q);
   st256(proof + (size_t)i * 64, c);
   st256(proof + (size_t)i * 64 + 32, v);
 }
@@ -996,9 +1003,13 @@ __global__ void k_response(const uint8_t* __restrict__ q_be, const uint8_t* __re
 // scalar derivation for the verifier (one thread per selection / contest)
 //   sel: out[i] = (q - c1_i) mod q  ; ok[i] = all of c0,v0,c1,v1 < q
 //   con: out[i] = (q - L*c_i mod q) ; ok[i] = c,v < q
-__global__ void k_scalar_prep(const uint8_t* __restrict__ q_be, const uint8_t* __restrict__ proofs,
+// plus (EG_RESPONSE_PLUS, a = g^v X^-c): out[i] = L*c_i mod q, and the proof words in neg_mask
+// (the challenges the variable bases are raised to) are negated in place, so the same job tables
+// compute X^-c; the Fiat-Shamir check then reads the caller's unmodified proofs.
+__global__ void k_scalar_prep(const uint8_t* __restrict__ q_be, uint8_t* __restrict__ proofs,
                               uint32_t n, uint32_t words_per, uint32_t neg_idx, uint32_t L,
-                              uint8_t* __restrict__ out, uint8_t* __restrict__ ok) {
+                              uint8_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t plus,
+                              uint32_t neg_mask) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const U256 q = ld256(q_be);
@@ -1007,7 +1018,13 @@ __global__ void k_scalar_prep(const uint8_t* __restrict__ q_be, const uint8_t* _
   U256 c = ld256(proofs + ((size_t)i * words_per + neg_idx) * 32);
   if (good) {
     if (L != 1) c = mulsmall_mod(c, L, q);
-    c = negmod(c, q);
+    if (!plus) c = negmod(c, q);
+    if (plus)
+      for (uint32_t k = 0; k < words_per; ++k)
+        if ((neg_mask >> k) & 1u) {
+          uint8_t* w = proofs + ((size_t)i * words_per + k) * 32;
+          st256(w, negmod(ld256(w), q));
+        }
   } else {
     for (int k = 0; k < 8; ++k) c.w[k] = 0;
   }
@@ -1021,6 +1038,8 @@ __global__ void k_scalar_prep(const uint8_t* __restrict__ q_be, const uint8_t* _
 //   minimal-length per hash_minimal (eg_ctx_set_hash_format).
 //   selection: elements (qbar, alpha, beta, a0, b0, a1, b1), expect (c0 + c1) mod q
 //   contest  : elements (qbar, A, B, a, b),                   expect c
+// (the elements after qbar in the ctx's pre-image order, eg_ctx_set_proof_format; up to 8 sources;
+// a source of stride 0 is one element shared by every proof, e.g. the election key K)
 // ---------------------------------------------------------------------------------
 struct HashSrc {
   const uint8_t* ptr;  // base pointer
@@ -1031,7 +1050,7 @@ struct HashSrc {
 __global__ void __launch_bounds__(kBlock) k_hash_check(const uint8_t* __restrict__ q_be,
                                                        const uint8_t* __restrict__ qbar_be, uint32_t n,
                                                        uint32_t nsrc, HashSrc s0, HashSrc s1, HashSrc s2,
-                                                       HashSrc s3, HashSrc s4, HashSrc s5,
+                                                       HashSrc s3, HashSrc s4, HashSrc s5, HashSrc s6, HashSrc s7,
                                                        const uint8_t* __restrict__ proofs,
                                                        uint32_t proof_words, uint32_t cidx0, uint32_t cidx1,
                                                        const uint8_t* __restrict__ pre_ok,
@@ -1049,7 +1068,7 @@ __global__ void __launch_bounds__(kBlock) k_hash_check(const uint8_t* __restrict
   H.put('|');
   H.put_hex(qbar_be, 32, hash_minimal != 0);
   H.put('|');
-  const HashSrc src[6] = {s0, s1, s2, s3, s4, s5};
+  const HashSrc src[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
   for (uint32_t k = 0; k < nsrc; ++k) {
     H.put_hex(src[k].ptr + (size_t)i * src[k].stride, src[k].bytes, hash_minimal != 0);
     H.put('|');

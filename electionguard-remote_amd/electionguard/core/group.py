@@ -270,6 +270,26 @@ class GroupContext:
         native.check(self._lib, "eg_ctx_set_hash_format", self._lib.eg_ctx_set_hash_format(self._ctx, FORMATS[fmt]))
         self._hash_format = fmt
 
+    # ---- response convention and challenge pre-image order (unpinned upstream, eg_ctx_set_proof_format) ----
+    RESPONSES = {"minus": 0, "plus": 1}
+    PREIMAGES = {"message_first": 0, "commitments_first": 1, "with_key": 2}
+
+    @property
+    def proof_format(self) -> tuple:
+        """(response, preimage): ("minus", "message_first") by default -- v = u - c x with a = g^v X^c,
+        and the hashed elements after Q-bar message first; see include/eg_hip.h for the variants."""
+        return getattr(self, "_proof_format", ("minus", "message_first"))
+
+    @proof_format.setter
+    def proof_format(self, fmt) -> None:
+        resp, pre = fmt
+        if resp not in self.RESPONSES or pre not in self.PREIMAGES:
+            raise ValueError(f"unknown proof format {fmt!r} (responses {list(self.RESPONSES)}, "
+                             f"pre-images {list(self.PREIMAGES)})")
+        native.check(self._lib, "eg_ctx_set_proof_format",
+                     self._lib.eg_ctx_set_proof_format(self._ctx, self.RESPONSES[resp], self.PREIMAGES[pre]))
+        self._proof_format = (resp, pre)
+
     # ---- constant-time encryption (eg_ctx_set_ct_encrypt) ----
     @property
     def ct_encrypt(self) -> bool:

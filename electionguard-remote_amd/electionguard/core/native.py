@@ -28,6 +28,7 @@ EXPORTED = [
     "eg_powp_one", "eg_gpowp_one", "eg_multp_one", "eg_ctx_set_ct_encrypt",
     "eg_dev_alloc", "eg_dev_free", "eg_memcpy_htod", "eg_memcpy_dtoh", "eg_memset_dev", "eg_all_nonzero_dev",
     "eg_comm_unique_id", "eg_comm_init", "eg_comm_destroy", "eg_comm_all_valid", "eg_tally_allgather_fold",
+    "eg_ctx_set_proof_format",
 ]
 
 
@@ -66,6 +67,7 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_clock_median": ([P, S, D, ctypes.POINTER(U32), ctypes.POINTER(U32)], I),
         "eg_ctx_g_table": ([P], P),
         "eg_ctx_set_hash_format": ([P, I], I),
+        "eg_ctx_set_proof_format": ([P, I, I], I),
         "eg_fixed_base_create": ([P, P, I, ctypes.POINTER(c_vp)], I),
         "eg_fixed_base_destroy": ([P], I),
         "eg_powp_batch": ([P, P, P, P, S], I),

@@ -100,6 +100,24 @@ eg_fixed_base* eg_ctx_g_table(eg_ctx* ctx);
 #define EG_HASH_MINIMAL 1
 int eg_ctx_set_hash_format(eg_ctx* ctx, int format);
 
+/* The two other unpinned proof conventions (upstream 1.0-SNAPSHOT's are not in the container;
+ * common.proto:23-28 pins only the field names "c" and "v"), switchable per context like the hex
+ * form; every proof this ctx makes or checks (range, constant, trustee share) follows them:
+ *   response: EG_RESPONSE_MINUS (default): v = u - c*x, checked as a = g^v X^c (eg_oracle.py);
+ *             EG_RESPONSE_PLUS: v = u + c*x, checked as g^v = a X^c (ElectionGuard 1.0's spec form);
+ *   preimage: the hashed elements after Q-bar --
+ *     EG_PREIMAGE_MESSAGE_FIRST (default): (alpha, beta, a0, b0, a1, b1) / (A, B, a, b) / (pad, data, a, b, M);
+ *     EG_PREIMAGE_COMMITMENTS_FIRST: (a0, b0, a1, b1, alpha, beta) / (a, b, A, B) / (a, b, pad, data, M);
+ *     EG_PREIMAGE_WITH_KEY: the public key first, (K, alpha, beta, ...) / (K, A, B, a, b) /
+ *                           (K_i, pad, data, a, b, M) with K_i = g^secret for a share.
+ * tools/pin_format.py reports which combination (with the hex form) verifies a given record. */
+#define EG_RESPONSE_MINUS 0
+#define EG_RESPONSE_PLUS 1
+#define EG_PREIMAGE_MESSAGE_FIRST 0
+#define EG_PREIMAGE_COMMITMENTS_FIRST 1
+#define EG_PREIMAGE_WITH_KEY 2
+int eg_ctx_set_proof_format(eg_ctx* ctx, int response, int preimage);
+
 /* Fixed-base radix table (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit
  * windows).  window_bits in [4, 22]; table = ceil(256/w) * 2^w elements of 640 B
  * in HBM (w = 16: 671 MB, w = 22: 32 GB). */

@@ -189,6 +189,56 @@ def hash_elems(q: int, *elems: Tuple[str, int]) -> int:
     return int.from_bytes(hashlib.sha256(msg).digest(), "big") % q
 
 
+# The two other unpinned proof conventions, switchable like the hex form (eg_ctx_set_proof_format):
+#   RESPONSE "minus" (default): v = u - c x, checked as a = g^v X^c;
+#            "plus": v = u + c x, checked as g^v = a X^c (a = g^v X^-c) -- ElectionGuard 1.0's spec form;
+#   PREIMAGE (the hashed elements after Q-bar):
+#            "message_first" (default): message, commitments, extra -- (alpha, beta, a0, b0, a1, b1),
+#                                       (A, B, a, b), (pad, data, a, b, M);
+#            "commitments_first": commitments, message, extra;
+#            "with_key": the public key (K; the guardian's K_i = g^s for a share), message, commitments,
+#                        extra.
+# Tests switch them with `with proof_format("plus", "with_key"):`.
+RESPONSES = ("minus", "plus")
+PREIMAGES = ("message_first", "commitments_first", "with_key")
+RESPONSE, PREIMAGE = "minus", "message_first"
+
+
+class proof_format:
+    def __init__(self, response: str = "minus", preimage: str = "message_first"):
+        assert response in RESPONSES and preimage in PREIMAGES
+        self.fmt = (response, preimage)
+
+    def __enter__(self):
+        global RESPONSE, PREIMAGE
+        self.prev, (RESPONSE, PREIMAGE) = (RESPONSE, PREIMAGE), self.fmt
+
+    def __exit__(self, *exc):
+        global RESPONSE, PREIMAGE
+        RESPONSE, PREIMAGE = self.prev
+
+
+def _resp_exp(q: int, c: int) -> int:
+    """The exponent the public base is raised to when recomputing a commitment: c (minus: a = g^v X^c)
+    or -c (plus: a = g^v X^-c)."""
+    return c % q if RESPONSE == "minus" else (-c) % q
+
+
+def _response(q: int, u: int, c: int, x: int) -> int:
+    return (u - c * x) % q if RESPONSE == "minus" else (u + c * x) % q
+
+
+def challenge(q: int, qbar: int, key: int, msg: Sequence[int], comm: Sequence[int], extra: Sequence[int] = ()) -> int:
+    """H(Q-bar, elements in the PREIMAGE order) mod q; every element an ElementModP."""
+    if PREIMAGE == "message_first":
+        els = [*msg, *comm, *extra]
+    elif PREIMAGE == "commitments_first":
+        els = [*comm, *msg, *extra]
+    else:
+        els = [key, *msg, *comm, *extra]
+    return hash_elems(q, ("Q", qbar), *(("P", e) for e in els))
+
+
 # --------------------------------------------------------------------------------------
 # ElGamal + Chaum-Pedersen (compact (c, v) proofs: common.proto:23-28)
 # --------------------------------------------------------------------------------------
@@ -220,18 +270,19 @@ def encrypt(G: Group, K: int, m: int, R: int) -> Ciphertext:
 
 
 def range_commitments(G: Group, K: int, ct: Ciphertext, pr: RangeProof) -> Tuple[int, int, int, int]:
-    """Verifier recompute: a_j = g^{v_j} alpha^{c_j}, b_j = K^{v_j} (beta g^-j)^{c_j}."""
-    p, q = G.p, G.q
-    a0 = G.multP(G.gPowP(pr.v0), G.powP(ct.pad, pr.c0))
-    b0 = G.multP(G.powP(K, pr.v0), G.powP(ct.data, pr.c0))
-    a1 = G.multP(G.gPowP(pr.v1), G.powP(ct.pad, pr.c1))
-    b1 = G.prodP([G.powP(K, pr.v1), G.powP(ct.data, pr.c1), G.gPowP((q - pr.c1) % q)])
+    """Verifier recompute: a_j = g^{v_j} alpha^{e_j}, b_j = K^{v_j} (beta g^-j)^{e_j}, e_j = c_j
+    (RESPONSE minus) or -c_j (plus)."""
+    q = G.q
+    e0, e1 = _resp_exp(q, pr.c0), _resp_exp(q, pr.c1)
+    a0 = G.multP(G.gPowP(pr.v0), G.powP(ct.pad, e0))
+    b0 = G.multP(G.powP(K, pr.v0), G.powP(ct.data, e0))
+    a1 = G.multP(G.gPowP(pr.v1), G.powP(ct.pad, e1))
+    b1 = G.prodP([G.powP(K, pr.v1), G.powP(ct.data, e1), G.gPowP((q - e1) % q)])
     return a0, b0, a1, b1
 
 
-def range_challenge(G: Group, qbar: int, ct: Ciphertext, a0: int, b0: int, a1: int, b1: int) -> int:
-    return hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data),
-                      ("P", a0), ("P", b0), ("P", a1), ("P", b1))
+def range_challenge(G: Group, qbar: int, ct: Ciphertext, a0: int, b0: int, a1: int, b1: int, K: int = 0) -> int:
+    return challenge(G.q, qbar, K, (ct.pad, ct.data), (a0, b0, a1, b1))
 
 
 def make_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, m: int, R: int,
@@ -240,16 +291,17 @@ def make_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, m: int, R: int
     q = G.q
     f = 1 - m
     a_real, b_real = G.gPowP(u), G.powP(K, u)
-    # fake branch f: a_f = g^{v_f} alpha^{c_f}, b_f = K^{v_f} (beta g^{-f})^{c_f}
-    a_fake = G.multP(G.gPowP(v_fake), G.powP(ct.pad, c_fake))
-    b_fake = G.prodP([G.powP(K, v_fake), G.powP(ct.data, c_fake), G.gPowP((q - f * c_fake) % q)])
+    # fake branch f: a_f = g^{v_f} alpha^{e_f}, b_f = K^{v_f} (beta g^{-f})^{e_f}, e_f = +-c_f
+    ef = _resp_exp(q, c_fake)
+    a_fake = G.multP(G.gPowP(v_fake), G.powP(ct.pad, ef))
+    b_fake = G.prodP([G.powP(K, v_fake), G.powP(ct.data, ef), G.gPowP((q - f * ef) % q)])
     if m == 0:
         a0, b0, a1, b1 = a_real, b_real, a_fake, b_fake
     else:
         a0, b0, a1, b1 = a_fake, b_fake, a_real, b_real
-    c = range_challenge(G, qbar, ct, a0, b0, a1, b1)
+    c = range_challenge(G, qbar, ct, a0, b0, a1, b1, K)
     c_real = (c - c_fake) % q
-    v_real = (u - c_real * R) % q
+    v_real = _response(q, u, c_real, R)
     if m == 0:
         return RangeProof(c_real, v_real, c_fake, v_fake)
     return RangeProof(c_fake, v_fake, c_real, v_real)
@@ -269,25 +321,26 @@ def verify_range_proof(G: Group, K: int, qbar: int, ct: Ciphertext, pr: RangePro
     if not all(0 <= x < q for x in (pr.c0, pr.v0, pr.c1, pr.v1)):
         return False
     a0, b0, a1, b1 = range_commitments(G, K, ct, pr)
-    return (pr.c0 + pr.c1) % q == range_challenge(G, qbar, ct, a0, b0, a1, b1)
+    return (pr.c0 + pr.c1) % q == range_challenge(G, qbar, ct, a0, b0, a1, b1, K)
 
 
 def constant_commitments(G: Group, K: int, A: int, B: int, limit: int, pr: GenericProof) -> Tuple[int, int]:
     q = G.q
-    a = G.multP(G.gPowP(pr.v), G.powP(A, pr.c))
-    b = G.prodP([G.powP(K, pr.v), G.powP(B, pr.c), G.gPowP((q - (limit * pr.c) % q) % q)])
+    e = _resp_exp(q, pr.c)
+    a = G.multP(G.gPowP(pr.v), G.powP(A, e))
+    b = G.prodP([G.powP(K, pr.v), G.powP(B, e), G.gPowP((q - (limit * e) % q) % q)])
     return a, b
 
 
-def constant_challenge(G: Group, qbar: int, A: int, B: int, a: int, b: int) -> int:
-    return hash_elems(G.q, ("Q", qbar), ("P", A), ("P", B), ("P", a), ("P", b))
+def constant_challenge(G: Group, qbar: int, A: int, B: int, a: int, b: int, K: int = 0) -> int:
+    return challenge(G.q, qbar, K, (A, B), (a, b))
 
 
 def make_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, R_sum: int, u: int) -> GenericProof:
     q = G.q
     a, b = G.gPowP(u), G.powP(K, u)
-    c = constant_challenge(G, qbar, A, B, a, b)
-    return GenericProof(c, (u - c * R_sum) % q)
+    c = constant_challenge(G, qbar, A, B, a, b, K)
+    return GenericProof(c, _response(q, u, c, R_sum))
 
 
 def verify_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, limit: int, pr: GenericProof) -> bool:
@@ -297,7 +350,7 @@ def verify_constant_proof(G: Group, K: int, qbar: int, A: int, B: int, limit: in
     if not (0 <= pr.c < G.q and 0 <= pr.v < G.q):
         return False
     a, b = constant_commitments(G, K, A, B, limit, pr)
-    return pr.c == constant_challenge(G, qbar, A, B, a, b)
+    return pr.c == constant_challenge(G, qbar, A, B, a, b, K)
 
 
 # --------------------------------------------------------------------------------------
@@ -500,12 +553,20 @@ def direct_decrypt(G: Group, qbar: int, gd: Guardian, texts: Sequence[Ciphertext
                    nonces: Sequence[int]) -> List[Tuple[int, GenericProof]]:
     """DirectDecryptionAndProof per text: M_i = A^{s_i} + generic CP proof
     (decrypting_trustee_rpc.proto:25-28)."""
+    return [(M, pr) for M, pr in share_proofs(G, qbar, gd.s, texts, nonces)]
+
+
+def share_proofs(G: Group, qbar: int, secret: int, texts: Sequence[Ciphertext],
+                 nonces: Sequence[int]) -> List[Tuple[int, GenericProof]]:
+    """M = pad^secret and its generic CP proof per text: a = g^u, b = pad^u,
+    c = H(qbar, [K_i = g^secret,] pad, data, a, b, M) (PREIMAGE order), v = u -+ c secret (RESPONSE)."""
+    Ki = G.gPowP(secret) if PREIMAGE == "with_key" else 0
     out = []
     for ct, u in zip(texts, nonces):
-        M = G.powP(ct.pad, gd.s)
+        M = G.powP(ct.pad, secret)
         a, b = G.gPowP(u), G.powP(ct.pad, u)
-        c = hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data), ("P", a), ("P", b), ("P", M))
-        out.append((M, GenericProof(c, (u - c * gd.s) % G.q)))
+        c = challenge(G.q, qbar, Ki, (ct.pad, ct.data), (a, b), (M,))
+        out.append((M, GenericProof(c, _response(G.q, u, c, secret))))
     return out
 
 
@@ -519,19 +580,14 @@ def compensated_decrypt(G: Group, qbar: int, gd: Guardian, missing: Guardian,
     """CompensatedDecryptionAndProof (decrypting_trustee_rpc.proto:41-45)."""
     share = poly_eval(missing.coeffs, gd.x, G.q)
     rk = recovery_public_key(G, missing, gd.x)
-    out = []
-    for ct, u in zip(texts, nonces):
-        M = G.powP(ct.pad, share)
-        a, b = G.gPowP(u), G.powP(ct.pad, u)
-        c = hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data), ("P", a), ("P", b), ("P", M))
-        out.append((M, GenericProof(c, (u - c * share) % G.q), rk))
-    return out
+    return [(M, pr, rk) for M, pr in share_proofs(G, qbar, share, texts, nonces)]
 
 
 def verify_share(G: Group, qbar: int, Ki: int, ct: Ciphertext, M: int, pr: GenericProof) -> bool:
-    a = G.multP(G.gPowP(pr.v), G.powP(Ki, pr.c))
-    b = G.multP(G.powP(ct.pad, pr.v), G.powP(M, pr.c))
-    return pr.c == hash_elems(G.q, ("Q", qbar), ("P", ct.pad), ("P", ct.data), ("P", a), ("P", b), ("P", M))
+    e = _resp_exp(G.q, pr.c)
+    a = G.multP(G.gPowP(pr.v), G.powP(Ki, e))
+    b = G.multP(G.powP(ct.pad, pr.v), G.powP(M, e))
+    return pr.c == challenge(G.q, qbar, Ki, (ct.pad, ct.data), (a, b), (M,))
 
 
 def lagrange(xs: Sequence[int], xi: int, q: int) -> int:

@@ -136,7 +136,65 @@ def spoiled(G):
     return out
 
 
-if __name__ == "__main__":
+def proof_formats(G):
+    """Every unpinned proof convention (eg_ctx_set_proof_format): the response sign x the challenge
+    pre-image order.  The same key, ballots, nonces and trustee texts under each variant (so the
+    variants differ only in proof bytes): 2 ballots of 2 x (2 + 1) and 3 texts' direct and
+    compensated shares (2 of 3 guardians available)."""
+    rng = random.Random(505)
+    gs, K = O.key_ceremony(G, 3, 2, rng)
+    qbar = rng.randrange(G.q)
+    man = O.Manifest(2, 2, 1)
+    plan = []
+    for _ in range(2):
+        votes = O.ballot_plaintexts(man, rng)
+        plan.append((votes, rng.getstate()))
+        O.encrypt_ballot(G, K, qbar, man, votes, rng)  # advance rng past this ballot's nonces
+    texts = [O.encrypt(G, K, rng.randrange(4), rng.randrange(1, G.q)) for _ in range(3)]
+    nonces = [rng.randrange(1, G.q) for _ in texts]
+    out = {"K": hx(K, 512), "qbar": hx(qbar, 32), "manifest": [2, 2, 1],
+           "guardians": [{"x": g.x, "coeffs": [hx(a, 32) for a in g.coeffs],
+                          "commitments": [hx(k, 512) for k in g.commitments]} for g in gs],
+           "texts": [[hx(t.pad, 512), hx(t.data, 512)] for t in texts], "nonces": [hx(u, 32) for u in nonces],
+           "variants": []}
+    for resp in O.RESPONSES:
+        for pre in O.PREIMAGES:
+            with O.proof_format(resp, pre):
+                v = {"response": resp, "preimage": pre, "ballots": []}
+                for votes, state in plan:
+                    r = random.Random()
+                    r.setstate(state)
+                    eb = O.encrypt_ballot(G, K, qbar, man, votes, r)
+                    r2 = random.Random()
+                    r2.setstate(state)
+                    nonces4, cnonces = [], []
+                    for c in range(man.n_contests):
+                        for s in range(man.sel_per_contest):
+                            nonces4.append([hx(r2.randrange(1, G.q), 32)] + [hx(r2.randrange(1, G.q), 32)] +
+                                           [hx(r2.randrange(G.q), 32), hx(r2.randrange(G.q), 32)])
+                        cnonces.append(hx(r2.randrange(1, G.q), 32))
+                    assert O.verify_ballot(G, K, qbar, man, eb)
+                    v["ballots"].append({
+                        "votes": votes, "nonces": nonces4, "contest_nonces": cnonces,
+                        "cts": [[hx(ct.pad, 512), hx(ct.data, 512)] for ct in eb.cts],
+                        "rproofs": [[hx(x, 32) for x in (pr.c0, pr.v0, pr.c1, pr.v1)] for pr in eb.proofs],
+                        "cproofs": [[hx(pr.c, 32), hx(pr.v, 32)] for pr in eb.contest_proofs]})
+                d = O.direct_decrypt(G, qbar, gs[0], texts, nonces)
+                c = O.compensated_decrypt(G, qbar, gs[1], gs[2], texts, nonces)
+                assert all(O.verify_share(G, qbar, gs[0].K, t, M, p) for t, (M, p) in zip(texts, d))
+                assert all(O.verify_share(G, qbar, rk, t, M, p) for t, (M, p, rk) in zip(texts, c))
+                v["direct"] = [{"M": hx(M, 512), "c": hx(p.c, 32), "v": hx(p.v, 32)} for M, p in d]
+                v["compensated_by_x2_for_x3"] = [{"M": hx(M, 512), "c": hx(p.c, 32), "v": hx(p.v, 32),
+                                                  "recovery": hx(rk, 512)} for M, p, rk in c]
+                out["variants"].append(v)
+    return out
+
+
+if __name__ == "__main__" and sys.argv[1:] == ["--proof-formats"]:
+    G = O.production_group(O.MODE4096)
+    (HERE / O.MODE4096 / "proof_formats.json").write_text(json.dumps(proof_formats(G), indent=0))
+    print("written proof_formats.json")
+elif __name__ == "__main__":
     for mode in (O.MODE4096, O.MODE4096_V2):
         out = HERE / mode
         out.mkdir(exist_ok=True)
@@ -145,6 +203,8 @@ if __name__ == "__main__":
         (out / "ballots.json").write_text(json.dumps(ballots(G), indent=0))
         (out / "trustee.json").write_text(json.dumps(trustee(G), indent=0))
         (out / "spoiled.json").write_text(json.dumps(spoiled(G), indent=0))
+        if mode == O.MODE4096:
+            (out / "proof_formats.json").write_text(json.dumps(proof_formats(G), indent=0))
         p, q, g, r = O.derive_group(mode)
         (out / "constants.json").write_text(json.dumps({"mode": mode, "p": hx(p, 512), "q": hx(q, 32),
                                                         "g": hx(g, 512), "r": hx(r, 512)}, indent=0))

@@ -1,0 +1,34 @@
+"""Report which proof conventions an upstream-produced record uses (see electionguard/formats.py):
+verifies its wire-layout ballots and trustee shares on the GPU under every combination of the hash
+pre-image hex form, the response sign and the pre-image order.
+
+    python tools/pin_format.py record.json        # prints one JSON line per combination, then the verdict
+"""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "electionguard-remote_amd"))
+
+
+def main(argv):
+    if len(argv) != 1:
+        sys.exit(__doc__)
+    from electionguard.core import productionGroup
+    from electionguard.formats import pin_formats
+    rec = json.loads(Path(argv[0]).read_text())
+    res = pin_formats(productionGroup(0), rec)
+    for r in res:
+        print(json.dumps(r))
+    hits = [r for r in res if r["all_valid"]]
+    if len(hits) == 1:
+        h = hits[0]
+        print(f"pinned: hash_format={h['hash_format']} response={h['response']} preimage={h['preimage']}")
+    else:
+        print(f"not pinned: {len(hits)} combinations verify everything")
+    return 0 if len(hits) == 1 else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
