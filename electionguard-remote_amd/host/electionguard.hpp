@@ -320,6 +320,10 @@ class GroupContext {
   // Fiat-Shamir pre-image hex form (EG_HASH_FIXED_WIDTH default / EG_HASH_MINIMAL): upstream's
   // is unpinned, so it is switchable per context (include/eg_hip.h).
   void setHashFormat(int format) const { check(eg_ctx_set_hash_format(ctx_, format), "eg_ctx_set_hash_format"); }
+  // response convention (EG_RESPONSE_MINUS / _PLUS) and challenge pre-image order (EG_PREIMAGE_*)
+  void setProofFormat(int response, int preimage) const {
+    check(eg_ctx_set_proof_format(ctx_, response, preimage), "eg_ctx_set_proof_format");
+  }
   const ElementModP& P() const { return p_; }
   const ElementModP& G() const { return g_; }
   const ElementModQ& Q() const { return q_; }

@@ -158,6 +158,11 @@ JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_setHashFormat(JNIEnv* env, j
 
 /* ---------------------------------------------------------------- fixed-base tables */
 
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_setProofFormat(JNIEnv* env, jclass cls, jlong ctx, jint response,
+                                                                   jint preimage) {
+  check_rc(env, eg_ctx_set_proof_format((eg_ctx*)(intptr_t)ctx, response, preimage));
+}
+
 JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_fixedBaseCreate(JNIEnv* env, jclass cls, jlong ctx,
                                                                      jbyteArray base, jint wbits) {
   if (need_len(env, base, EG_P_BYTES, 0, "base: 512 bytes")) return 0;

@@ -56,6 +56,10 @@ public final class EgHip {
 
   public static native void setHashFormat(long ctx, int format);
 
+  /** Response convention (0 = v = u - c x, 1 = v = u + c x) and challenge pre-image order
+   *  (0 message first, 1 commitments first, 2 public key first): eg_ctx_set_proof_format. */
+  public static native void setProofFormat(long ctx, int response, int preimage);
+
   // ---- fixed-base tables (PowRadix / acceleratePow; LOW_MEMORY_USE = 8-bit windows) ----
   public static native long fixedBaseCreate(long ctx, byte[] base512, int windowBits);
 

@@ -165,6 +165,8 @@ int main(void) {
   EXPECT("gTable(0)", NULL);
   Java_electionguard_gpu_EgHip_setHashFormat(env, C, N0, 0);
   EXPECT("setHashFormat(0)", AE);
+  Java_electionguard_gpu_EgHip_setProofFormat(env, C, N0, 1, 2);
+  EXPECT("setProofFormat(0)", AE);
   Java_electionguard_gpu_EgHip_setCtEncrypt(env, C, N0, 1);
   EXPECT("setCtEncrypt(0)", AE);
   {
