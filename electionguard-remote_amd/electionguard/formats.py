@@ -6,8 +6,10 @@ format common.proto:23-28 pins only the field names "c" and "v".)
 layouts: 512-byte ElementModP, 32-byte ElementModQ, big-endian) on the GPU under every combination
 of the three switchable conventions -- the hash pre-image's hex form (eg_ctx_set_hash_format), the
 response sign and the challenge pre-image order (eg_ctx_set_proof_format) -- and reports the
-combinations under which everything verifies.  Proofs made under one combination fail under every
-other (a different challenge or a different commitment), so an honest record pins exactly one.
+combinations under which everything verifies.  Proofs made under one response / pre-image order
+fail under every other (a different challenge or a different commitment), so an honest record pins
+both; the two hex forms hash the same text unless a hashed element has a leading zero byte (about
+1 element in 256 for random 4096-bit values), so a small record may leave the hex form open.
 
 Record (JSON, hex strings; tools/pin_format.py):
   {"K": ..., "qbar": ..., "manifest": [contests, selections, votes_allowed],
@@ -87,4 +89,15 @@ def pin_formats(group, rec: dict) -> List[Dict]:
             out.append(r)
     finally:
         group.hash_format, group.proof_format = saved
+    return out
+
+
+def summarize(results: List[Dict]) -> Dict:
+    """-> {"response", "preimage", "hash_format"}: each a name when every combination that verifies
+    everything agrees on it, None when nothing verifies, "undetermined" when several values do."""
+    hits = [r for r in results if r["all_valid"]]
+    out = {}
+    for k in ("response", "preimage", "hash_format"):
+        vals = sorted({r[k] for r in hits})
+        out[k] = vals[0] if len(vals) == 1 else (None if not vals else "undetermined")
     return out

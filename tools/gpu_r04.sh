@@ -20,6 +20,11 @@ if [[ $STEPS == *gloo2* ]]; then
     --modexp-n 4096 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo2.log 2>&1
   echo "gloo2: $(tail -c 300 gpurun_out/${TAG}_rehearse_gloo2.log)"
 fi
+if [[ $STEPS == *ftest* ]]; then
+  timeout -k 10 600 python -u -m pytest ${FTESTS} -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/${TAG}_gpu_tests_focus.log 2>&1
+  echo "ftest: $(tail -n 1 gpurun_out/${TAG}_gpu_tests_focus.log)"
+fi
 if [[ $STEPS == *ptest* ]]; then
   timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_comm.py -m gpu -x -v --timeout 300 \
     --timeout-method thread > gpurun_out/${TAG}_gpu_tests_pipeline.log 2>&1

@@ -16,18 +16,15 @@ def main(argv):
     if len(argv) != 1:
         sys.exit(__doc__)
     from electionguard.core import productionGroup
-    from electionguard.formats import pin_formats
+    from electionguard.formats import pin_formats, summarize
     rec = json.loads(Path(argv[0]).read_text())
     res = pin_formats(productionGroup(0), rec)
     for r in res:
         print(json.dumps(r))
-    hits = [r for r in res if r["all_valid"]]
-    if len(hits) == 1:
-        h = hits[0]
-        print(f"pinned: hash_format={h['hash_format']} response={h['response']} preimage={h['preimage']}")
-    else:
-        print(f"not pinned: {len(hits)} combinations verify everything")
-    return 0 if len(hits) == 1 else 1
+    s = summarize(res)
+    print("pinned:" if s["response"] not in (None, "undetermined") and s["preimage"] not in (None, "undetermined")
+          else "not pinned:", json.dumps(s))
+    return 0 if s["response"] not in (None, "undetermined") and s["preimage"] not in (None, "undetermined") else 1
 
 
 if __name__ == "__main__":
