@@ -51,8 +51,10 @@ static_assert(kN * kLimbBits >= 4098, "R must exceed 4p (lazy reduction: values 
 // Accumulator headroom: a register lives L steps in its lane and takes <= 2 products per step
 // (x*y + m*p; with SQR one doubled x*x product + m*p).  Radix 2^29 needs L <= 18.
 static_assert((unsigned __int128)2 * kL * (((1ull << kLimbBits) + 64) * ((1ull << kLimbBits) + 64)) < ((unsigned __int128)1 << 64), "radix 2^29 overflows the 64-bit columns above 18 limbs per lane");
-static_assert(kT == 4 || kT == 8, "EG_T must be 4 or 8");
-static_assert(kW == 160, "device element format is 160 words");
+// kT = 16 (one DPP row per element, 9 limbs per lane) is the latency-shaped instantiation of
+// eg_pow16.hip (the per-element coalescer's small batches); its element format is 192 words
+static_assert(kT == 4 || kT == 8 || kT == 16, "EG_T must be 4, 8 or 16");
+static_assert(kW == (kT == 16 ? 192 : 160), "device element format is 160 words (192 for T = 16)");
 
 // Device constants of one group context (filled by the host, eg_capi.hip).
 struct MontConsts {
@@ -87,6 +89,7 @@ __device__ __forceinline__ uint32_t bcast_g0(uint32_t v) {
   // bit-mode swizzle within 32 lanes: lane' = lane & and_mask (clears the in-group bits)
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, kT == 8 ? 0x0018 : 0x001C);
 #else
+  if constexpr (kT == 16) return __builtin_amdgcn_mov_dpp(v, 0x150 /*row_newbcast:0*/, 0xF, 0xF, false);
   uint32_t a = __builtin_amdgcn_mov_dpp(v, 0x00 /*quad_perm [0,0,0,0]*/, 0xF, 0xF, false);
   if constexpr (kT == 8) {
     // lanes 4-7 / 12-15 of every row take the value 4 lanes below (the group's lane 0)
@@ -122,6 +125,8 @@ __device__ __forceinline__ uint32_t bcast_g0_and(uint32_t v, uint32_t mask) {
 #elif EG_BCAST == 1
   return bcast_g0(v) & mask;
 #else
+  // T = 16: the group is a DPP row, one row_newbcast:0 move (gfx90a+) broadcasts its lane 0
+  if constexpr (kT == 16) return __builtin_amdgcn_mov_dpp(v, 0x150 /*row_newbcast:0*/, 0xF, 0xF, true) & mask;
   // AND first on the full-mask quad_perm move (the DPP combiner folds it into
   // v_and_b32_dpp when mask is a VGPR), then the half-row move for T = 8
   uint32_t a = __builtin_amdgcn_mov_dpp(v, 0x00 /*quad_perm [0,0,0,0]*/, 0xF, 0xF, true) & mask;

@@ -29,6 +29,7 @@
 
 #include "../../include/eg_hip.h"
 #include "eg_kernels.hpp"
+#include "eg_pow16.h"
 
 using namespace eg;
 
@@ -210,6 +211,11 @@ struct eg_ctx {
   hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
   void* comm = nullptr;  // RCCL communicator of the multi-GPU exchange (eg_comm_init; eg_capi_comm.inc)
   int comm_world = 1, comm_rank = 0;
+  // the 16-lane latency-shaped powP (eg_pow16.hip) for the coalescer's small batches: its constants,
+  // the elements one resident round of it holds (batches up to that size take it), and the switch
+  // (EG_LATENCY_POW=0 keeps every batch on the 8-lane layout, for A/B runs)
+  Pow16Consts* lat = nullptr;
+  size_t lat_jobs = 0;
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
 
@@ -696,6 +702,11 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   c->h.n0 = (0u - inv) & kMask;
   c->h.friendly = c->h.n0 == 1 ? 1u : 0u;
   c->h.mask = kMask;
+  if (!(getenv("EG_LATENCY_POW") && getenv("EG_LATENCY_POW")[0] == '0')) {
+    std::string err;
+    if (pow16_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->lat, &err) == 0)
+      c->lat_jobs = pow16_round_jobs(device);
+  }
   {  // c = 2^256 - q (mod 2^256) for the residue test x^(2^256) == x^c
     const Big q = be_to_words(q_be, 32);
     int64_t br = 0;
@@ -781,6 +792,7 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
     if (r.b) hipEventDestroy(r.b);
   }
   if (c->d_clk) hipFree(c->d_clk);
+  pow16_consts_destroy(c->lat);
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);

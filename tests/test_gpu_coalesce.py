@@ -47,6 +47,38 @@ def test_cpp_eleven_threads_per_element_bitexact(group, tmp_path):
     assert res["powp_submit_wait_per_s"] > 0.25 * res["powp_batch_per_s"]
 
 
+def test_latency_shape_for_blocking_callers(group, tmp_path):
+    """The coalescer's small powP batches run on the 16-lane layout (eg_pow16.hip): bit-exact on the
+    edge cases, and 11 blocking per-element callers get their results faster than on the 8-lane
+    layout (EG_LATENCY_POW=0 keeps every batch there); one blocking caller is dispatched at once
+    (the window ends when the previous batch's callers are back)."""
+    import os
+    import eg_oracle as O
+    og = O.production_group()
+    rng = random.Random(41)
+    n = 660
+    recs = []
+    for i in range(n):
+        b = rng.randrange(og.p) if i % 5 else rng.choice([0, 1, og.p - 1, og.p, og.p + 1, 2**4096 - 1])
+        e = rng.randrange(og.q) if i % 9 else rng.choice([0, 1, 2, og.q - 1, og.q, 2**256 - 1])
+        recs.append(b.to_bytes(512, "big") + e.to_bytes(32, "big") + pow(b, e, og.p).to_bytes(512, "big") +
+                    bytes(512) + bytes(512) + pow(og.g, e, og.p).to_bytes(512, "big"))
+    vec = tmp_path / "vectors.bin"
+    vec.write_bytes(struct.pack("<I", n) + b"".join(recs))
+    res = {}
+    for shape, env in (("16-lane", {}), ("8-lane", {"EG_LATENCY_POW": "0"})):
+        for threads in (11, 1):
+            r = subprocess.run([str(BIN), str(vec), str(threads)], capture_output=True, text=True, timeout=600,
+                               env=dict(os.environ, **env))
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            res[(shape, threads)] = d
+    print({k: (v["powp_one_blocking_per_s"], v["mismatches"]) for k, v in res.items()})
+    for (shape, threads), d in res.items():
+        assert d["mismatches"] == 0, (shape, threads, d)  # (the multP vectors are a x 0 = 0)
+    assert res[("16-lane", 11)]["powp_one_blocking_per_s"] > 1.3 * res[("8-lane", 11)]["powp_one_blocking_per_s"]
+    assert res[("16-lane", 1)]["powp_one_blocking_per_s"] > 1.3 * res[("8-lane", 1)]["powp_one_blocking_per_s"]
+
+
 def test_python_threads_per_element_bitexact(group):
     from electionguard.core.group import ElementModP, ElementModQ
     rng = random.Random(23)
