@@ -201,7 +201,11 @@ public final class GpuGroupContext implements AutoCloseable {
     return elementP(out, 0);
   }
 
-  /** base.powP(e) queued now, completed by the library's next batch. */
+  /**
+   * base.powP(e) queued now, completed by the library's next batch.  The waits run on this context's
+   * own daemon threads (never ForkJoinPool.commonPool: many outstanding waits there would starve
+   * unrelated parallel streams and CompletableFutures of the JVM).
+   */
   public java.util.concurrent.CompletableFuture<ElementModP> powPAsync(ElementModP base, ElementModQ e) {
     byte[] b = new byte[EgHip.P_BYTES], x = new byte[EgHip.Q_BYTES];
     put(b, 0, base.byteArray(), EgHip.P_BYTES);
@@ -211,8 +215,15 @@ public final class GpuGroupContext implements AutoCloseable {
       byte[] out = new byte[EgHip.P_BYTES];
       EgHip.ticketWait(t, out);
       return elementP(out, 0);
-    });
+    }, waiters);
   }
+
+  // the threads that wait for submitted tickets (a blocked wait holds one; idle ones exit after 30 s)
+  private final java.util.concurrent.ExecutorService waiters = java.util.concurrent.Executors.newCachedThreadPool(r -> {
+    Thread th = new Thread(r, "eg-hip-ticket-wait");
+    th.setDaemon(true);
+    return th;
+  });
 
   /** Batch window of the per-element calls (defaults: 16384 elements, 100 us). */
   public void setCoalescing(long maxBatch, int windowUs) { EgHip.setCoalescing(ctx, maxBatch, windowUs); }

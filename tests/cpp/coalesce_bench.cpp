@@ -112,9 +112,35 @@ int main(int argc, char** argv) {
     const ElementModQ e = ElementModQ::from_be(rec(0) + 512);
     bad += std::memcmp(b.powP(e).byteArray(), rec(0) + 544, 512) != 0;
   }
-  printf("{\"n\": %u, \"threads\": %d, \"mismatches\": %ld, \"powp_batch_per_s\": %.1f, "
+  // 5. batch latency sweep: one submit-all-then-wait batch of m elements through the coalescer
+  // (max_batch = m: dispatched as soon as the m-th arrives) and one eg_powp_batch call of m, best of 3
+  std::string sweep;
+  for (uint32_t m : {1u, 11u, 64u, 256u, 1024u, 4096u, 12288u}) {
+    if (m > n) m = n;
+    std::vector<uint8_t> O3((size_t)m * 512);
+    double co_best = 1e9, b_best = 1e9;
+    check(eg_ctx_set_coalescing(ctx, m, 1000000), "eg_ctx_set_coalescing");
+    for (int rep = 0; rep < 4; ++rep) {  // the first is a warm-up (job tables, buffers)
+      std::vector<eg_ticket*> ts(m);
+      auto t = Clock::now();
+      for (uint32_t i = 0; i < m; ++i) check(eg_powp_submit(ctx, rec(i % n), rec(i % n) + 512, &O3[(size_t)i * 512], &ts[i]), "submit");
+      for (auto* x : ts) bad += eg_ticket_wait(x) != EG_OK;
+      if (rep) co_best = std::min(co_best, secs(t));
+      t = Clock::now();
+      check(eg_powp_batch(ctx, B.data(), E.data(), O.data(), m), "eg_powp_batch");
+      if (rep) b_best = std::min(b_best, secs(t));
+    }
+    for (uint32_t i = 0; i < m; ++i) bad += std::memcmp(&O3[(size_t)i * 512], rec(i % n) + 544, 512) != 0;
+    char buf[160];
+    snprintf(buf, sizeof buf, "%s{\"m\": %u, \"coalesced_ms\": %.3f, \"batch_call_ms\": %.3f}", sweep.empty() ? "" : ", ", m,
+             co_best * 1e3, b_best * 1e3);
+    sweep += buf;
+    if (m == n) break;
+  }
+  check(eg_ctx_set_coalescing(ctx, 16384, 100), "eg_ctx_set_coalescing");
+  printf("{\"n\": %u, \"threads\": %d, \"mismatches\": %ld, \"sweep\": [%s], \"powp_batch_per_s\": %.1f, "
          "\"powp_one_blocking_per_s\": %.1f, \"multp_one_blocking_per_s\": %.1f, \"gpowp_one_blocking_per_s\": %.1f, "
          "\"powp_submit_wait_per_s\": %.1f}\n",
-         n, nthreads, bad.load(), n / batch_s, n / one_powp_s, n / one_multp_s, n / one_gpowp_s, n / async_s);
+         n, nthreads, bad.load(), sweep.c_str(), n / batch_s, n / one_powp_s, n / one_multp_s, n / one_gpowp_s, n / async_s);
   return bad.load() == 0 ? 0 : 1;
 }

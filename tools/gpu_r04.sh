@@ -25,6 +25,10 @@ if [[ $STEPS == *ftest* ]]; then
     > gpurun_out/${TAG}_gpu_tests_focus.log 2>&1
   echo "ftest: $(tail -n 1 gpurun_out/${TAG}_gpu_tests_focus.log)"
 fi
+if [[ $STEPS == *shapes* ]]; then
+  timeout -k 10 900 python tools/coalesce_shapes.py > gpurun_out/${TAG}_coalesce_shapes.json 2> gpurun_out/${TAG}_coalesce_shapes.err
+  echo "shapes: $(grep -E 'blocking|crossover' gpurun_out/${TAG}_coalesce_shapes.json | tr -d '\n')"
+fi
 if [[ $STEPS == *ptest* ]]; then
   timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_comm.py -m gpu -x -v --timeout 300 \
     --timeout-method thread > gpurun_out/${TAG}_gpu_tests_pipeline.log 2>&1
