@@ -194,6 +194,7 @@ struct eg_ctx {
   eg_fixed_base* g_ct = nullptr;  // g's kCtEncWindow-bit table (K's live in keys[].ct)
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
   uint32_t sel_rows = 4;                // verifier selection jobs' comb: 4 = 4 rows x 3 blocks, 0 = 5 rows x 2 blocks (EG_SEL_COMB=52)
+  uint32_t sel_blocks = 3;              // its column blocks (EG_SEL_COMB=42 / 44: 4 rows x 2 / 4 blocks, A/B only)
   // k_pow workgroups resident at once (CUs x blocks per CU): the verifier sizes its launch
   // populations so launches end on full rounds (EG_TAIL_SPLIT=0 disables; 0 = unknown)
   size_t pow_slots = 0;
@@ -480,8 +481,8 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   // every population of the launch: its shape and the buffers it needs
   auto check = [&](const PowShape& X, const uint32_t* yg, const uint32_t* ro, const uint32_t* ct_tab) {
     if (X.resid && (!X.comb || X.gather || !ro)) return fail(EG_ERR_ARG, "residue pairs need a plain comb shape and rout");
-    if (X.blocks > 1 && (X.blocks > 3 || !X.comb || X.gather || X.shared_comb))
-      return fail(EG_ERR_ARG, "two or three column blocks need a plain comb shape");
+    if (X.blocks > 1 && (X.blocks > 4 || !X.comb || X.gather || X.shared_comb))
+      return fail(EG_ERR_ARG, "two to four column blocks need a plain comb shape");
     if (X.shared_comb && (!X.comb || X.gather || X.resid || !ct_tab)) return fail(EG_ERR_ARG, "shared comb table missing");
     if (X.rows && (X.rows != 4 || !X.comb || X.gather || X.shared_comb))
       return fail(EG_ERR_ARG, "4-row combs are plain comb shapes");
@@ -721,7 +722,10 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   }
   if (const char* nc = getenv("EG_NO_COMB")) c->use_comb = (nc[0] == '1') ? 0u : 1u;
   if (const char* cr = getenv("EG_CT_ROWS")) c->ct_rows = (cr[0] == '5') ? 0u : 4u;
-  if (const char* sc = getenv("EG_SEL_COMB")) c->sel_rows = (sc[0] == '5') ? 0u : 4u;
+  if (const char* sc = getenv("EG_SEL_COMB")) {
+    c->sel_rows = (sc[0] == '5') ? 0u : 4u;
+    c->sel_blocks = (sc[0] == '5') ? 2u : (sc[1] == '2' ? 2u : (sc[1] == '4' ? 4u : 3u));
+  }
   if (const char* tf = getenv("EG_TEST_FAIL_JOBS")) c->test_fail_jobs = atoi(tf);
   if (const char* cw = getenv("EG_CT_WINDOW")) c->ct_window = std::max(4, std::min((int)kCtMaxWindow, atoi(cw)));
   {

@@ -18,12 +18,15 @@ BUILD = ROOT / "tools" / "_ab"
 
 
 def build(name, flags):
+    if not flags.strip():  # no -D flags: the in-tree library (run-time switches only, e.g. name@sel42)
+        return ROOT / "electionguard-remote_amd" / "electionguard" / "lib" / "libeg_hip.so"
     BUILD.mkdir(exist_ok=True)
     out = BUILD / f"libeg_{name}.so"
-    if not out.exists():
+    if not out.exists():  # both translation units (the 8-lane core and the 16-lane eg_pow16.hip)
+        csrc = ROOT / "electionguard-remote_amd" / "csrc"
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
                "-Wno-unused-result", "-Wno-pass-failed", *flags.split(), "-I", str(ROOT / "include"), "-o", str(out),
-               str(ROOT / "electionguard-remote_amd" / "csrc" / "eg_capi.hip")]
+               str(csrc / "eg_capi.hip"), str(csrc / "eg_pow16.hip")]
         subprocess.run(cmd, check=True)
     return out
 
@@ -130,8 +133,9 @@ if __name__ == "__main__":
             env_extra["EG_CB_EARLY"] = "0"
         if "@cbe" in name:  # early contest-b jobs in launch 2 (opt-in schedule)
             env_extra["EG_CB_EARLY"] = "1"
-        if "@sel43" in name:  # verifier selection jobs on the 4-row, 3-block comb
-            env_extra["EG_SEL_COMB"] = "43"
+        for sel in ("43", "42", "44", "52"):  # verifier selection jobs' comb: rows x column blocks
+            if f"@sel{sel}" in name:
+                env_extra["EG_SEL_COMB"] = sel
         if "@l3w" in name:  # with @cbe: launch 3 sized to 1..3 waves per SIMD (default 2)
             env_extra["EG_CB_EARLY"] = "1"
             env_extra["EG_L3_WAVES"] = name.split("@l3w")[1][:1]

@@ -29,6 +29,12 @@ if [[ $STEPS == *shapes* ]]; then
   timeout -k 10 900 python tools/coalesce_shapes.py > gpurun_out/${TAG}_coalesce_shapes.json 2> gpurun_out/${TAG}_coalesce_shapes.err
   echo "shapes: $(grep -E 'blocking|crossover' gpurun_out/${TAG}_coalesce_shapes.json | tr -d '\n')"
 fi
+if [[ $STEPS == *abcomb* ]]; then
+  # interleaved same-box A/B of the verifier's selection comb (rows x column blocks), per shader clock
+  AB_MODE=verify AB_NB=10000 AB_WB=22 timeout -k 10 900 python tools/ab_mm.py cur= cur@sel42= cur@sel44= cur= \
+    cur@sel42= cur@sel44= cur= cur@sel42= cur@sel44= > gpurun_out/${TAG}_ab_selcomb.log 2>&1
+  echo "abcomb: $(tail -c 600 gpurun_out/${TAG}_ab_selcomb.log)"
+fi
 if [[ $STEPS == *ptest* ]]; then
   timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_comm.py -m gpu -x -v --timeout 300 \
     --timeout-method thread > gpurun_out/${TAG}_gpu_tests_pipeline.log 2>&1
