@@ -35,6 +35,11 @@ if [[ $STEPS == *abcomb* ]]; then
     cur@sel42= cur@sel44= cur= cur@sel42= cur@sel44= > gpurun_out/${TAG}_ab_selcomb.log 2>&1
   echo "abcomb: $(tail -c 600 gpurun_out/${TAG}_ab_selcomb.log)"
 fi
+if [[ $STEPS == *rccl* ]]; then
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29541 tools/rccl_selfcheck.py > gpurun_out/${TAG}_rccl_selfcheck.log 2>&1
+  echo "rccl: $(tail -n 2 gpurun_out/${TAG}_rccl_selfcheck.log)"
+fi
 if [[ $STEPS == *ptest* ]]; then
   timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_comm.py -m gpu -x -v --timeout 300 \
     --timeout-method thread > gpurun_out/${TAG}_gpu_tests_pipeline.log 2>&1
