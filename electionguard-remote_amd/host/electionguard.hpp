@@ -915,6 +915,80 @@ inline VerifyResult verifyBallots(const GroupContext& G, const ElementModP& K, c
   return r;
 }
 
+// ---- device memory and the multi-GPU tally exchange (include/eg_hip.h eg_dev_* / eg_comm_*) ----
+// HBM on the context's device through the library's own HIP runtime (RAII).
+class DeviceBuffer {
+ public:
+  DeviceBuffer(const GroupContext& G, size_t bytes) : ctx_(G.handle()), bytes_(bytes) {
+    check(eg_dev_alloc(ctx_, bytes, &ptr_), "eg_dev_alloc");
+  }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  ~DeviceBuffer() { eg_dev_free(ctx_, ptr_); }
+  uint8_t* data() const { return (uint8_t*)ptr_; }
+  size_t size() const { return bytes_; }
+  void upload(const void* src, size_t bytes, size_t offset = 0) {
+    if (offset + bytes > bytes_) throw std::out_of_range("DeviceBuffer::upload past the end");
+    check(eg_memcpy_htod(ctx_, data() + offset, src, bytes), "eg_memcpy_htod");
+  }
+  void download(void* dst, size_t bytes, size_t offset = 0) const {
+    if (offset + bytes > bytes_) throw std::out_of_range("DeviceBuffer::download past the end");
+    check(eg_memcpy_dtoh(ctx_, dst, data() + offset, bytes), "eg_memcpy_dtoh");
+  }
+  bool allNonzero(size_t n) const {  // the first n bytes are non-zero flags (verifier verdicts)
+    int all = 0;
+    check(eg_all_nonzero_dev(ctx_, data(), n, &all), "eg_all_nonzero_dev");
+    return all != 0;
+  }
+
+ private:
+  eg_ctx* ctx_;
+  void* ptr_ = nullptr;
+  size_t bytes_;
+};
+
+// One rank's RCCL communicator inside the library: rank 0 makes the id, the caller
+// sends it to every rank over any host channel, each rank constructs the exchange (collective).
+class TallyExchange {
+ public:
+  static std::array<uint8_t, EG_COMM_ID_BYTES> uniqueId() {
+    std::array<uint8_t, EG_COMM_ID_BYTES> id{};
+    check(eg_comm_unique_id(id.data()), "eg_comm_unique_id");
+    return id;
+  }
+  TallyExchange(const GroupContext& G, const uint8_t id[EG_COMM_ID_BYTES], int world, int rank)
+      : G_(G), rank_(rank) {
+    check(eg_comm_init(G.handle(), id, world, rank), "eg_comm_init");
+  }
+  TallyExchange(const TallyExchange&) = delete;
+  TallyExchange& operator=(const TallyExchange&) = delete;
+  ~TallyExchange() { eg_comm_destroy(G_.handle()); }
+  bool allValid(bool ok) const {
+    int all = 0;
+    check(eg_comm_all_valid(G_.handle(), ok ? 1 : 0, &all), "eg_comm_all_valid");
+    return all != 0;
+  }
+  // every rank's nparts x n partial-tally rows in HBM, folded mod p; the product on root, empty elsewhere
+  std::vector<ElementModP> fold(const DeviceBuffer& parts, size_t nparts, size_t n, int root = 0) const {
+    return foldTally(G_, parts, nparts, n, root, rank_);
+  }
+  static std::vector<ElementModP> foldTally(const GroupContext& G, const DeviceBuffer& parts, size_t nparts, size_t n,
+                                            int root = 0, int rank = 0) {
+    if (parts.size() < nparts * n * EG_P_BYTES) throw std::out_of_range("fold: parts shorter than nparts x n");
+    std::vector<uint8_t> out(n * EG_P_BYTES);
+    check(eg_tally_allgather_fold(G.handle(), parts.data(), nparts, n, root, rank == root ? out.data() : nullptr),
+          "eg_tally_allgather_fold");
+    if (rank != root) return {};
+    std::vector<ElementModP> r(n);
+    for (size_t i = 0; i < n; ++i) r[i] = ElementModP(&out[i * EG_P_BYTES], &G);
+    return r;
+  }
+
+ private:
+  const GroupContext& G_;
+  int rank_;
+};
+
 // Decryption.decryptBallot (RunRemoteDecryptor.java:264-269) over a batch of spoiled ballots:
 // every ballot's real selections (placeholders are not part of the plaintext) go to the trustees
 // as ONE batch per guardian, then the same share checks, Lagrange combine and dLog (<= votes

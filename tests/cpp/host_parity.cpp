@@ -8,6 +8,7 @@
 // Prints "OK <checks>" and exits 0, or prints the first mismatch and exits 1.
 #include <cstdio>
 #include <fstream>
+#include <random>
 #include <iostream>
 #include <sstream>
 
@@ -275,6 +276,33 @@ static int run_gpu(const char* path, ProductionMode mode) {
     EXPECT(!chk.tally && chk.directProofs, "negative count flagged");
     // dLogG above the bound -> not found
     EXPECT(!G.dLogG(G.gPowP(G.uIntToElementModQ(1500)), 1000).has_value(), "dLogG beyond maxResult");
+  }
+  {  // device memory and the tally exchange: 3 local parts folded, then RCCL at world size 1
+    std::mt19937_64 rng(77);
+    const size_t n = 9, nparts = 3;
+    std::vector<ElementModP> xs;
+    for (size_t i = 0; i < n * nparts; ++i) xs.push_back(G.gPowP(G.randomElementModQ(rng)));
+    const auto raw = GroupContext::packP(xs);
+    DeviceBuffer d(G, raw.size());
+    d.upload(raw.data(), raw.size());
+    std::vector<uint8_t> back(raw.size());
+    d.download(back.data(), back.size());
+    EXPECT(back == raw, "device buffer round trip");
+    auto folded = TallyExchange::foldTally(G, d, nparts, n);
+    for (size_t k = 0; k < n; ++k)
+      EXPECT(folded[k] == G.multP({xs[k], xs[n + k], xs[2 * n + k]}), "local fold of 3 parts, element " << k);
+    const auto id = TallyExchange::uniqueId();
+    TallyExchange x(G, id.data(), 1, 0);
+    EXPECT(x.allValid(true) && !x.allValid(false), "RCCL verdict all-reduce at world 1");
+    folded = x.fold(d, nparts, n);
+    for (size_t k = 0; k < n; ++k) EXPECT(folded[k] == G.multP({xs[k], xs[n + k], xs[2 * n + k]}), "RCCL fold " << k);
+    std::vector<uint8_t> flags(100, 1);
+    DeviceBuffer df(G, flags.size());
+    df.upload(flags.data(), flags.size());
+    EXPECT(df.allNonzero(flags.size()), "flags all set");
+    flags[99] = 0;
+    df.upload(flags.data(), flags.size());
+    EXPECT(!df.allNonzero(flags.size()) && df.allNonzero(99), "a zero flag found");
   }
   std::cout << "OK " << g_checks << std::endl;
   return 0;
