@@ -228,6 +228,16 @@ public final class GpuGroupContext implements AutoCloseable {
   /** Batch window of the per-element calls (defaults: 16384 elements, 100 us). */
   public void setCoalescing(long maxBatch, int windowUs) { EgHip.setCoalescing(ctx, maxBatch, windowUs); }
 
+  /** Hash pre-image hex form: 0 = fixed width (default), 1 = minimal (eg_ctx_set_hash_format). */
+  public void setHashFormat(int format) { EgHip.setHashFormat(ctx, format); }
+
+  /**
+   * Response convention (0: v = u - c x, 1: v = u + c x) and challenge pre-image order (0 message
+   * first, 1 commitments first, 2 public key first) of every proof made or checked on this context;
+   * tools/pin_format.py finds the combination an upstream record uses (eg_ctx_set_proof_format).
+   */
+  public void setProofFormat(int response, int preimage) { EgHip.setProofFormat(ctx, response, preimage); }
+
   // ------------------------------------------------------------------ ballots
 
   /** Verdicts and tally of {@link #verifyBallots}. */
