@@ -134,6 +134,8 @@ static int run_gpu(const char* path, ProductionMode mode) {
     } else if (op == "multInv") {
       ia.push_back(ElementModP::from_hex(t[1], &G));
       ir.push_back(ElementModP::from_hex(t[2], &G));
+    } else if (op == "format") {  // response convention and pre-image order of what follows
+      G.setProofFormat(std::stoi(t[1]), std::stoi(t[2]));
     } else if (op == "prodP") {
       std::vector<ElementModP> xs;
       for (size_t i = 2; i < t.size(); ++i) xs.push_back(ElementModP::from_hex(t[i], &G));
@@ -304,6 +306,7 @@ static int run_gpu(const char* path, ProductionMode mode) {
     df.upload(flags.data(), flags.size());
     EXPECT(!df.allNonzero(flags.size()) && df.allNonzero(99), "a zero flag found");
   }
+  G.setProofFormat(EG_RESPONSE_MINUS, EG_PREIMAGE_MESSAGE_FIRST);
   std::cout << "OK " << g_checks << std::endl;
   return 0;
 }

@@ -71,3 +71,32 @@ def test_cpp_host_gpu_parity(tmp_path, mode):
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("OK")
+
+
+def write_format_vectors(path: Path, variant: dict, fx: dict) -> None:
+    """The trustee lines of one proof-format variant (tests/golden/Mode4096/proof_formats.json)."""
+    resp = {"minus": 0, "plus": 1}[variant["response"]]
+    pre = {"message_first": 0, "commitments_first": 1, "with_key": 2}[variant["preimage"]]
+    lines = [f"format {resp} {pre}"]
+    for gd in fx["guardians"]:
+        lines.append(f"guardian {gd['x']} {len(gd['coeffs'])} " + " ".join(gd["coeffs"]) + " " +
+                     " ".join(gd["commitments"]))
+    lines.append(f"qbar {fx['qbar']}")
+    lines += [f"text {a} {b}" for a, b in fx["texts"]]
+    lines += [f"nonce {u}" for u in fx["nonces"]]
+    lines += [f"direct {d['M']} {d['c']} {d['v']}" for d in variant["direct"]]
+    lines += [f"compensated {d['M']} {d['c']} {d['v']} {d['recovery']}" for d in variant["compensated_by_x2_for_x3"]]
+    path.write_text("\n".join(lines) + "\n")
+
+
+@pytest.mark.gpu
+def test_cpp_host_proof_formats(tmp_path):
+    """GroupContext::setProofFormat: the C++ trustee reproduces every variant's shares and proofs, and
+    the 5-guardian decryption (proofs made and checked under that variant) recovers its counts."""
+    fx = json.loads((GOLD / "Mode4096" / "proof_formats.json").read_text())
+    for v in fx["variants"]:
+        f = tmp_path / f"{v['response']}_{v['preimage']}.txt"
+        write_format_vectors(f, v, fx)
+        r = subprocess.run([str(_bin()), "gpu", str(f)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (v["response"], v["preimage"], r.stdout + r.stderr)
+        assert r.stdout.startswith("OK")
