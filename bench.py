@@ -256,6 +256,8 @@ def verify_tally(a, world, rank, local, dist):
     value = nb * world * a.steps / el
     out = line_common(a, world, el, value, kp, nb, man, "ballots verified+tallied/sec (node, 4096-bit group)",
                       xch.collective)
+    if xch.note:
+        out["config"]["exchange_note"] = xch.note
     out["modexp_per_s_per_gpu"] = {"var_base": modexp.get("var_base_per_s"),
                                    "fixed_base_g": modexp.get("fixed_base_g_per_s")} if modexp else None
     # a derived count, not a measurement: the verify step's work expressed in 256-bit
@@ -616,6 +618,8 @@ def full_pipeline(a, world, rank, local, dist, keep=None):
     out = line_common(a, world, el, value, kp, nb, man,
                       "ballots encrypted+verified+tallied+decrypted/sec (node, 4096-bit group, full pipeline)",
                       xch.collective)
+    if xch.note:
+        out["config"]["exchange_note"] = xch.note
     tot = nb * world * a.steps
     out["phases"] = {
         "encrypt": {"s": round(phases["encrypt"], 3), "ballots_per_s": round(tot / phases["encrypt"], 1)},

@@ -107,13 +107,41 @@ class TallyExchange:
     it on its GPU (prodP_groups); every rank may share one GPU.
     world 1: the local tally, through the same fold entry point (no communicator)."""
 
-    def __init__(self, group, dist, world: int, rank: int, mode: str = "rccl"):
+    def __init__(self, group, dist, world: int, rank: int, mode: str = "rccl", fallback: bool = True):
         if mode not in ("rccl", "gloo"):
             raise ValueError(f"unknown exchange mode {mode!r}")
         self.group, self.dist, self.world, self.rank, self.mode = group, dist, world, rank, mode
+        self.note = None
         if world > 1 and mode == "rccl":
-            uid = share_comm_id(dist, rank, group.comm_unique_id)
-            group.comm_init(uid, world, rank)
+            err = None
+            try:
+                uid = share_comm_id(dist, rank, group.comm_unique_id) if rank != 0 else None
+            except Exception as e:  # rank 0 broadcasts even when it could not make an id
+                err = e
+            if rank == 0:
+                try:
+                    uid = group.comm_unique_id()
+                except Exception as e:
+                    uid, err = b"", e  # the others' share_comm_id fails on it: nobody calls eg_comm_init
+                box = [uid]
+                dist.broadcast_object_list(box, src=0)
+            if err is None:
+                try:
+                    group.comm_init(uid, world, rank)
+                except Exception as e:
+                    err = e
+            # every rank learns whether every rank has a communicator; if one failed, the whole
+            # world keeps the exchange on the host (the line says so) instead of dying
+            if not all_valid(dist, err is None):
+                if fallback:
+                    if err is None:
+                        group.comm_destroy()
+                    self.mode = "gloo"
+                    self.note = f"RCCL communicator unavailable ({err or 'on another rank'}): host exchange"
+                    import sys
+                    print(f"rank {rank}: {self.note}", file=sys.stderr, flush=True)
+                else:
+                    raise RuntimeError(f"eg_comm_init failed: {err or 'on another rank'}")
 
     @property
     def collective(self) -> str:

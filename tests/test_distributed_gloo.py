@@ -213,3 +213,45 @@ def test_launcher_fails_fast_when_a_rank_dies(tmp_path):
     rc = run_ranks(str(child), [str(tmp_path / "unused.json")], 2, timeout=240, env=env)
     assert rc == 3
     assert time.monotonic() - t < 60
+
+
+def _fallback_worker(rank, world, port, q):
+    """TallyExchange in "rccl" mode where rank 1 cannot create its communicator: every rank
+    learns it and the whole world falls back to the host exchange (no rank dies, no rank hangs)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from electionguard.distributed import TallyExchange
+
+    class FakeGroup:
+        destroyed = False
+
+        @staticmethod
+        def comm_unique_id():
+            return bytes(range(128))
+
+        def comm_init(self, uid, w, r):
+            assert uid == bytes(range(128)) and w == world and r == rank
+            if rank == 1:
+                raise RuntimeError("no RCCL here")
+
+        def comm_destroy(self):
+            FakeGroup.destroyed = True
+
+    g = FakeGroup()
+    x = TallyExchange(g, dist, world, rank, "rccl")
+    q.put((rank, x.mode, x.collective, FakeGroup.destroyed, x.note is not None))
+    dist.destroy_process_group()
+
+
+def test_rccl_init_failure_falls_back_to_the_host_exchange():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [(0, "gloo", "gloo (host)", True, True), (1, "gloo", "gloo (host)", False, True)]
