@@ -212,11 +212,14 @@ struct eg_ctx {
   hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
   void* comm = nullptr;  // RCCL communicator of the multi-GPU exchange (eg_comm_init; eg_capi_comm.inc)
   int comm_world = 1, comm_rank = 0;
-  // the 16-lane latency-shaped powP (eg_pow16.hip) for the coalescer's small batches: its constants,
-  // the elements one resident round of it holds (batches up to that size take it), and the switch
-  // (EG_LATENCY_POW=0 keeps every batch on the 8-lane layout, for A/B runs)
+  // the latency-shaped powP layouts (eg_pow16.hip) for the coalescer's small batches: one element
+  // per wave for batches up to one per SIMD (latw_jobs), 16-lane groups up to one resident round
+  // (lat_jobs); EG_LATENCY_POW=0 keeps every batch on the 8-lane layout, =16 skips the per-wave one
+  // (A/B runs)
   Pow16Consts* lat = nullptr;
   size_t lat_jobs = 0;
+  PowWaveConsts* latw = nullptr;
+  size_t latw_jobs = 0;
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
 
@@ -703,10 +706,18 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   c->h.n0 = (0u - inv) & kMask;
   c->h.friendly = c->h.n0 == 1 ? 1u : 0u;
   c->h.mask = kMask;
-  if (!(getenv("EG_LATENCY_POW") && getenv("EG_LATENCY_POW")[0] == '0')) {
+  {
+    const char* lp = getenv("EG_LATENCY_POW");
+    const std::string mode = lp ? lp : "";
     std::string err;
-    if (pow16_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->lat, &err) == 0)
+    if (mode != "0" && pow16_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->lat, &err) == 0)
       c->lat_jobs = pow16_round_jobs(device);
+    if (mode != "0" && mode != "16" &&
+        powwave_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->latw, &err) == 0) {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
+        c->latw_jobs = (size_t)cus * 4;  // one element per SIMD
+    }
   }
   {  // c = 2^256 - q (mod 2^256) for the residue test x^(2^256) == x^c
     const Big q = be_to_words(q_be, 32);
@@ -797,6 +808,7 @@ extern "C" int eg_ctx_destroy(eg_ctx* c) {
   }
   if (c->d_clk) hipFree(c->d_clk);
   pow16_consts_destroy(c->lat);
+  powwave_consts_destroy(c->latw);
   if (c->d) hipFree(c->d);
   if (c->d_q) hipFree(c->d_q);
   if (c->d_qbar) hipFree(c->d_qbar);

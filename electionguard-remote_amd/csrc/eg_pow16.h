@@ -28,3 +28,16 @@ size_t pow16_round_jobs(int device);
 int pow16_powp(const Pow16Consts* C, bool friendly, hipStream_t s, const uint32_t* sched, const uint32_t* jobs,
                const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n, uint32_t* elems,
                uint32_t* outs, uint32_t* scratch, std::string* err);
+
+// One element per WAVE (eg_pow16.hip, namespace egw): 48 lanes x 3 limbs of 2^29 (the same 144
+// limbs and Montgomery radix), lanes 48-63 holding zeros, the quotient digit broadcast with
+// v_readlane and the limb shift a wave_shl:1 DPP move, 5-bit sliding-window exponent.  A batch of
+// up to one element per SIMD runs every element on its own SIMD: the shortest latency a blocking
+// per-element caller can get (the coalescer's smallest batches).
+struct PowWaveConsts;
+int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t* one, uint32_t n0, uint32_t friendly,
+                          PowWaveConsts** out, std::string* err);
+void powwave_consts_destroy(PowWaveConsts* c);
+// out_be[i] = base_be[i]^exp_be[i] mod p (device pointers, asynchronous on s; no scratch)
+int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint8_t* base_be, const uint8_t* exp_be,
+                 uint8_t* out_be, size_t n, std::string* err);

@@ -112,3 +112,255 @@ int pow16_powp(const Pow16Consts* C, bool friendly, hipStream_t s, const uint32_
   }
   return 0;
 }
+
+// =================================================================================================
+// One element per wave (egw): the latency shape for the smallest per-element batches.
+//   * 144 limbs of 2^29 over lanes 0-47, three per lane (lane l holds limbs 3l .. 3l+2), lanes
+//     48-63 hold zeros in x, y, p and the accumulator, so every lane runs the same code and the
+//     idle ones only ever pass zeros (the shift into lane 47 reads lane 48's zero, the final carry
+//     out of lane 47 is zero because the result is < 2p < R);
+//   * CIOS as eg_bignum.hpp's mont_mul_impl (the same rotating accumulator registers and the same
+//     split of the lowest column), but the quotient digit is ONE v_readlane of lane 0 (the whole
+//     wave is one element: no DPP broadcast), the multiplier digit y_s is a v_readlane of the lane
+//     that holds it, and the limb shift a wave_shl:1 DPP move;
+//   * the exponent is read by the whole wave (one element per wave), so a 5-bit sliding window
+//     (16 odd powers in LDS, ~314 Montgomery operations per 256-bit exponent against 329 for the
+//     fixed 4-bit window) keeps every branch wave-uniform.
+// =================================================================================================
+namespace egw {
+constexpr int kBits = 29, kLimbs = 144, kLL = 3, kLanes = 48, kRow = 64 * kLL;
+constexpr uint32_t kM = (1u << kBits) - 1u;
+static_assert(kLanes * kLL == kLimbs, "48 lanes x 3 limbs");
+
+struct Consts {
+  uint32_t p[kRow], r2[kRow], one[kRow];  // limb i at [i], zeros from 144 on
+  uint32_t n0;
+};
+
+__device__ __forceinline__ uint32_t lane64() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t wnext(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x130 /*wave_shl:1*/, 0xF, 0xF, true); }
+__device__ __forceinline__ uint32_t wprev(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x138 /*wave_shr:1*/, 0xF, 0xF, true); }
+
+// x <- x * y * R^-1 mod p (R = 2^4176), result < 2p with limbs < 2^29 + small; y may alias x
+template <bool F>
+__device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&p)[kLL], uint32_t n0) {
+  uint64_t acc[kLL] = {0, 0, 0};
+#pragma unroll 1
+  for (int q = 0; q < kLanes; ++q) {  // multiplier limbs 3q .. 3q+2 live in lane q
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) {
+      const uint32_t yi = __builtin_amdgcn_readlane(y[r], q);
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) {
+        uint64_t& A = acc[(j + r) % kLL];
+        A = (uint64_t)x[j] * yi + A;
+      }
+      uint32_t t0 = __builtin_amdgcn_readlane((uint32_t)acc[r], 0);  // the lowest column (lane 0)
+      if (!F) t0 *= n0;
+      const uint32_t m = t0 & kM;
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) {
+        uint64_t& A = acc[(j + r) % kLL];
+        A = (uint64_t)p[j] * m + A;
+      }
+      uint64_t& A0 = acc[r];
+      acc[(r + 1) % kLL] += A0 >> kBits;         // the carry stays in this lane's next column
+      A0 = (uint64_t)(wnext((uint32_t)A0) & kM);  // the low bits move to the lane below's top column
+    }
+  }
+  // two carry passes (the registers are back in natural order: 144 steps = 48 x 3)
+  uint64_t d[kLL];
+  {
+    const uint64_t top = acc[kLL - 1] >> kBits;
+    const uint64_t c_in = (uint64_t)wprev((uint32_t)top) | ((uint64_t)wprev((uint32_t)(top >> 32)) << 32);
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) d[j] = (uint64_t)((uint32_t)acc[j] & kM) + (j == 0 ? c_in : (acc[j - 1] >> kBits));
+  }
+  const uint32_t c_in = wprev((uint32_t)(d[kLL - 1] >> kBits));
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) x[j] = ((uint32_t)d[j] & kM) + (j == 0 ? c_in : (uint32_t)(d[j - 1] >> kBits));
+}
+
+// canonical form of a value in [0, p] (limbs as mul leaves them): carries rippled up through the
+// lanes until none is left (wave-uniform loop), then p -> 0
+__device__ __forceinline__ void normalize(uint32_t (&x)[kLL], const uint32_t (&p)[kLL], uint32_t ln) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) {
+    const uint32_t v = x[j] + c;
+    x[j] = v & kM;
+    c = v >> kBits;
+  }
+  for (int round = 0; round < 64; ++round) {
+    uint32_t cin = wprev(c);
+    if (__ballot(cin != 0) == 0) break;
+    c = 0;
+    if (cin) {
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) {
+        const uint32_t v = x[j] + cin;
+        x[j] = v & kM;
+        cin = v >> kBits;
+      }
+      c = cin;
+    }
+  }
+  bool eq = true;
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) eq &= x[j] == p[j];
+  if (__ballot(!eq) == 0) {
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) x[j] = 0;
+  }
+  (void)ln;
+}
+
+template <bool F>
+__global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, const uint8_t* __restrict__ base_be,
+                                                  const uint8_t* __restrict__ exp_be, uint8_t* __restrict__ out_be,
+                                                  uint32_t n) {
+  __shared__ uint32_t s_tab[16][kRow];  // x^1, x^3, ..., x^31 (Montgomery form)
+  __shared__ uint32_t s_w[kRow];        // byte <-> limb staging
+  __shared__ uint32_t s_e[8];           // the exponent, little-endian words
+  const uint32_t e = blockIdx.x;       // one element per workgroup of one wave; the grid is exactly n
+  if (e >= n) return;
+  const uint32_t ln = lane64();
+  const uint32_t n0 = C->n0;
+  uint32_t p[kLL], x[kLL], y[kLL];
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) p[j] = C->p[kLL * ln + j];
+  // 512 big-endian bytes -> 128 little-endian words -> this lane's three limbs
+  const uint32_t* be32 = reinterpret_cast<const uint32_t*>(base_be + (size_t)e * 512);
+  for (uint32_t k = ln; k < 128; k += 64) s_w[127 - k] = __builtin_bswap32(be32[k]);
+  if (ln < 8) s_e[7 - ln] = __builtin_bswap32(reinterpret_cast<const uint32_t*>(exp_be + (size_t)e * 32)[ln]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) {
+    const int bit = kBits * (kLL * (int)ln + j), wi = bit >> 5, sh = bit & 31;
+    const uint32_t lo = (ln < kLanes && wi < 128) ? s_w[wi] : 0u;
+    const uint32_t hi = (ln < kLanes && wi + 1 < 128) ? s_w[wi + 1] : 0u;
+    x[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & kM;
+    y[j] = C->r2[kLL * ln + j];
+  }
+  mul<F>(x, y, p, n0);  // Montgomery form (a base >= p is reduced here: x * R^2 * R^-1 < 2p)
+  // odd powers for the 5-bit sliding window
+  uint32_t x2[kLL] = {x[0], x[1], x[2]};
+  mul<F>(x2, x, p, n0);
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) s_tab[0][kLL * ln + j] = x[j];
+#pragma unroll 1
+  for (int k = 1; k < 16; ++k) {
+    mul<F>(x, x2, p, n0);
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = x[j];
+  }
+  __syncthreads();
+  // the exponent, read by the whole wave (readfirstlane: every branch below is wave-uniform)
+  auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_e[i >> 5]) >> (i & 31)) & 1u; };
+  int i = 255;
+  while (i >= 0 && !bit(i)) --i;
+  if (i < 0) {
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];  // x^0 = 1 (also 0^0)
+  } else {
+    bool started = false;
+    while (i >= 0) {
+      if (!bit(i)) {
+        mul<F>(x, x, p, n0);
+        --i;
+        continue;
+      }
+      int l = i - 4 < 0 ? 0 : i - 4;
+      while (!bit(l)) ++l;  // the window [i, l] ends on a set bit: an odd value
+      uint32_t val = 0;
+      for (int k = i; k >= l; --k) val = val << 1 | bit(k);
+      if (started)
+        for (int k = 0; k < i - l + 1; ++k) mul<F>(x, x, p, n0);
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) y[j] = s_tab[val >> 1][kLL * ln + j];
+      if (started) {
+        mul<F>(x, y, p, n0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kLL; ++j) x[j] = y[j];
+        started = true;
+      }
+      i = l - 1;
+    }
+  }
+  // leave the Montgomery domain (x * 1 * R^-1: a value in [0, p]) and write canonical bytes
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) y[j] = (ln == 0 && j == 0) ? 1u : 0u;
+  mul<F>(x, y, p, n0);
+  normalize(x, p, ln);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) s_w[kLL * ln + j] = x[j];
+  __syncthreads();
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out_be + (size_t)e * 512);
+  for (uint32_t b = ln; b < 128; b += 64) {  // big-endian word b = little-endian word 127 - b
+    const int bitpos = 32 * (127 - (int)b), a = bitpos / kBits, sh = bitpos - a * kBits;
+    auto limb = [&](int k) -> uint64_t { return k < kLimbs ? (uint64_t)s_w[k] : 0ull; };
+    const uint64_t v = (limb(a) >> sh) | (limb(a + 1) << (kBits - sh)) | (limb(a + 2) << (2 * kBits - sh));
+    out32[b] = __builtin_bswap32((uint32_t)v);
+  }
+}
+}  // namespace egw
+
+struct PowWaveConsts {
+  egw::Consts* d = nullptr;
+};
+
+int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t* one, uint32_t n0, uint32_t friendly,
+                          PowWaveConsts** out, std::string* err) {
+  (void)friendly;
+  egw::Consts h{};
+  auto limbs = [](const uint32_t* w, int nw, uint32_t* o) {
+    for (int a = 0; a < egw::kLimbs; ++a) {
+      const int bit = a * egw::kBits;
+      uint64_t v = 0;
+      for (int k = 0; k < 3; ++k) {
+        const int wi = bit / 32 + k;
+        if (wi < nw) v |= (uint64_t)w[wi] << (32 * k);
+      }
+      o[a] = (uint32_t)(v >> (bit % 32)) & egw::kM;
+    }
+  };
+  limbs(p, 128, h.p);
+  limbs(r2, 129, h.r2);
+  limbs(one, 129, h.one);
+  h.n0 = n0;
+  auto* c = new PowWaveConsts();
+  hipError_t e = hipMalloc(&c->d, sizeof(egw::Consts));
+  if (e == hipSuccess) e = hipMemcpy(c->d, &h, sizeof(egw::Consts), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (c->d) hipFree(c->d);
+    delete c;
+    *err = std::string("powwave constants: ") + hipGetErrorString(e);
+    return 1;
+  }
+  *out = c;
+  return 0;
+}
+
+void powwave_consts_destroy(PowWaveConsts* c) {
+  if (!c) return;
+  if (c->d) hipFree(c->d);
+  delete c;
+}
+
+int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint8_t* base_be, const uint8_t* exp_be,
+                 uint8_t* out_be, size_t n, std::string* err) {
+  if (!n) return 0;
+  if (friendly)
+    hipLaunchKernelGGL(egw::k_powp_wave<true>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be, (uint32_t)n);
+  else
+    hipLaunchKernelGGL(egw::k_powp_wave<false>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be,
+                       (uint32_t)n);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    *err = std::string("powwave launch: ") + hipGetErrorString(e);
+    return 1;
+  }
+  return 0;
+}

@@ -1,6 +1,7 @@
-"""Per-element powP through the coalescer on the two layouts (verdict r03 item 5): the 16-lane
-latency-shaped batches (eg_pow16.hip, the default for batches of one resident round) against the
-8-lane layout (EG_LATENCY_POW=0), for 11 and 1 blocking caller threads and a one-batch latency
+"""Per-element powP through the coalescer on its three layouts (verdict r03 item 5): one element per
+wave (eg_pow16.hip egw, the default for batches up to one element per SIMD), the 16-lane groups
+(EG_LATENCY_POW=16: small batches up to one resident round on eg16) and the 8-lane layout
+(EG_LATENCY_POW=0), for 11 and 1 blocking caller threads and a one-batch latency
 sweep, next to the host CPU's variable-base rate (the bench line's cpu_baseline
 var_base_modexp_per_s_per_core, OpenSSL BN_mod_exp_mont on one core) x 11 threads and x the lease's
 cores.  Expected results come from CPython pow (every result is checked by coalesce_bench).
@@ -44,7 +45,8 @@ def main():
         vec = Path(d) / "v.bin"
         vec.write_bytes(struct.pack("<I", a.n) + b"".join(recs))
         res = {}
-        for shape, env in (("16-lane", {}), ("8-lane", {"EG_LATENCY_POW": "0"})):
+        for shape, env in (("per-wave", {}), ("16-lane", {"EG_LATENCY_POW": "16"}),
+                           ("8-lane", {"EG_LATENCY_POW": "0"})):
             for threads in (11, 1):
                 r = subprocess.run([str(BIN), str(vec), str(threads)], capture_output=True, text=True, timeout=900,
                                    env=dict(os.environ, **env))
@@ -56,7 +58,7 @@ def main():
     out = {"n": a.n, "host_per_core_powp_per_s": a.per_core, "host_cores": a.cores,
            "host_11_threads_powp_per_s": cpu11, "host_all_cores_powp_per_s": cpu_all, "runs": res}
     # the batch size above which one GPU batch beats the host's cores on the same elements
-    for shape in ("16-lane", "8-lane"):
+    for shape in ("per-wave", "16-lane", "8-lane"):
         sweep = res[f"{shape}/11"]["sweep"]
         out[f"crossover_vs_{a.cores}_cores_{shape}"] = next(
             (s["m"] for s in sweep if s["m"] / (s["coalesced_ms"] / 1e3) > cpu_all), None)
