@@ -36,6 +36,7 @@ def _rec(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=12288)
+    ap.add_argument("--n-single", type=int, default=1024, help="elements of the one-caller runs")
     ap.add_argument("--per-core", type=float, default=1686.0, help="host variable-base powP/s on one core")
     ap.add_argument("--cores", type=int, default=16, help="the lease's usable host cores")
     a = ap.parse_args()
@@ -44,18 +45,24 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         vec = Path(d) / "v.bin"
         vec.write_bytes(struct.pack("<I", a.n) + b"".join(recs))
+        # one blocking caller pays the whole latency per element: a smaller set keeps each run short
+        n1 = min(a.n, a.n_single)
+        vec1 = Path(d) / "v1.bin"
+        vec1.write_bytes(struct.pack("<I", n1) + b"".join(recs[:n1]))
         res = {}
         for shape, env in (("per-wave", {}), ("16-lane", {"EG_LATENCY_POW": "16"}),
                            ("8-lane", {"EG_LATENCY_POW": "0"})):
             for threads in (11, 1):
-                r = subprocess.run([str(BIN), str(vec), str(threads)], capture_output=True, text=True, timeout=900,
-                                   env=dict(os.environ, **env))
+                r = subprocess.run([str(BIN), str(vec if threads > 1 else vec1), str(threads)], capture_output=True,
+                                   text=True, timeout=900, env=dict(os.environ, **env))
                 if r.returncode:
                     sys.exit(r.stdout + r.stderr)
                 res[f"{shape}/{threads}"] = json.loads(r.stdout.strip().splitlines()[-1])
+                print(f"{shape}/{threads}: {res[f'{shape}/{threads}']['powp_one_blocking_per_s']} powP/s blocking",
+                      file=sys.stderr, flush=True)
     cpu11 = a.per_core * 11
     cpu_all = a.per_core * a.cores
-    out = {"n": a.n, "host_per_core_powp_per_s": a.per_core, "host_cores": a.cores,
+    out = {"n": a.n, "n_single_caller": min(a.n, a.n_single), "host_per_core_powp_per_s": a.per_core, "host_cores": a.cores,
            "host_11_threads_powp_per_s": cpu11, "host_all_cores_powp_per_s": cpu_all, "runs": res}
     # the batch size above which one GPU batch beats the host's cores on the same elements
     for shape in ("per-wave", "16-lane", "8-lane"):
