@@ -12,6 +12,7 @@
 #undef eg
 
 #pragma clang diagnostic ignored "-Wunused-value"
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -134,7 +135,10 @@ static_assert(kLanes * kLL == kLimbs, "48 lanes x 3 limbs");
 
 struct Consts {
   uint32_t p[kRow], r2[kRow], one[kRow];  // limb i at [i], zeros from 144 on
+  // p + 1 with its limbs shifted down by 2 (pd) and by 1 (pd1): the delayed-quotient multiply
+  uint32_t pd[kRow], pd1[kRow];
   uint32_t n0;
+  uint32_t mask;  // 2^29 - 1, read at run time so the AND folds into the DPP limb shift (v_and_b32_dpp)
 };
 
 __device__ __forceinline__ uint32_t lane64() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -143,7 +147,8 @@ __device__ __forceinline__ uint32_t wprev(uint32_t v) { return __builtin_amdgcn_
 
 // x <- x * y * R^-1 mod p (R = 2^4176), result < 2p with limbs < 2^29 + small; y may alias x
 template <bool F>
-__device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&p)[kLL], uint32_t n0) {
+__device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&p)[kLL], uint32_t n0,
+                                    uint32_t mv) {
   uint64_t acc[kLL] = {0, 0, 0};
 #pragma unroll 1
   for (int q = 0; q < kLanes; ++q) {  // multiplier limbs 3q .. 3q+2 live in lane q
@@ -165,7 +170,7 @@ __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL]
       }
       uint64_t& A0 = acc[r];
       acc[(r + 1) % kLL] += A0 >> kBits;         // the carry stays in this lane's next column
-      A0 = (uint64_t)(wnext((uint32_t)A0) & kM);  // the low bits move to the lane below's top column
+      A0 = (uint64_t)(wnext((uint32_t)A0) & mv);  // the low bits move to the lane below's top column
     }
   }
   // two carry passes (the registers are back in natural order: 144 steps = 48 x 3)
@@ -179,6 +184,72 @@ __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL]
   const uint32_t c_in = wprev((uint32_t)(d[kLL - 1] >> kBits));
 #pragma unroll
   for (int j = 0; j < kLL; ++j) x[j] = ((uint32_t)d[j] & kM) + (j == 0 ? c_in : (uint32_t)(d[j - 1] >> kBits));
+}
+
+// The same product for p = -1 mod 2^58 (both production groups: p = -1 mod 2^256), with the quotient
+// digit off the step's dependency chain.  With p~ = p + 1 (limbs 0 and 1 zero), m*p = m*p~ - m, and the
+// "- m" is the retiring column's low 29 bits (= m), which the wave_shl drops anyway; m_i * p~_j lands in
+// column i + j >= i + 2, so it is applied two steps late (m_{i-2} against p~ shifted down by two limbs,
+// pd) and never feeds the next quotient's column: each step's chain is the lowest column's
+// MAC -> carry shift -> add, the readlane of the quotient runs beside it.  The quotient digits are the
+// standard CIOS ones (the m-terms of columns < i + 8 telescope to multiples of 2^29 for this p), so
+// the result is the same integer as mul<true>.  The last two digits are applied after the loop.
+__device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&pd)[kLL],
+                                       const uint32_t (&pd1)[kLL], uint32_t mv) {
+  uint64_t acc[kLL] = {0, 0, 0};
+  uint32_t m1 = 0, m2 = 0;  // quotient digits of the previous two steps
+#pragma unroll 1
+  for (int q = 0; q < kLanes; ++q) {
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) {
+      const uint32_t yi = __builtin_amdgcn_readlane(y[r], q);
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) {
+        uint64_t& A = acc[(j + r) % kLL];
+        A = (uint64_t)x[j] * yi + A;
+      }
+      // keep one v_mad_u64_u32 per product: without the barrier the compiler re-associates the
+      // early-known m2 terms into separate products plus 64-bit adds (r04h: 25% slower)
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) asm volatile("" : "+v"(acc[j]));
+      asm volatile("" : "+s"(m2));  // a 32-bit SGPR: otherwise the loop carries it widened to 64 bits (two MACs)
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) {
+        uint64_t& A = acc[(j + r) % kLL];
+        A = (uint64_t)pd[j] * m2 + A;
+      }
+      uint64_t& A0 = acc[r];
+      const uint32_t m = __builtin_amdgcn_readlane((uint32_t)A0, 0) & kM;
+      acc[(r + 1) % kLL] += A0 >> kBits;
+      A0 = (uint64_t)(wnext((uint32_t)A0) & mv);
+      m2 = m1;
+      m1 = m;
+    }
+  }
+  // the last two digits: after 144 steps position P holds column 144 + P, m_142 * p~_J belongs to
+  // P = J - 2 (pd) and m_143 * p~_J to P = J - 1 (pd1)
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) acc[j] = (uint64_t)pd[j] * m2 + acc[j];
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) acc[j] = (uint64_t)pd1[j] * m1 + acc[j];
+  uint64_t d[kLL];
+  {
+    const uint64_t top = acc[kLL - 1] >> kBits;
+    const uint64_t c_in = (uint64_t)wprev((uint32_t)top) | ((uint64_t)wprev((uint32_t)(top >> 32)) << 32);
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) d[j] = (uint64_t)((uint32_t)acc[j] & kM) + (j == 0 ? c_in : (acc[j - 1] >> kBits));
+  }
+  const uint32_t c_in = wprev((uint32_t)(d[kLL - 1] >> kBits));
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) x[j] = ((uint32_t)d[j] & kM) + (j == 0 ? c_in : (uint32_t)(d[j - 1] >> kBits));
+}
+
+// MODE 0: general p, 1: p = -1 mod 2^29 (n0 = 1), 2: p = -1 mod 2^58 (delayed quotient, mul_d2)
+template <int MODE>
+__device__ __forceinline__ void mulm(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&p)[kLL],
+                                     const uint32_t (&pd)[kLL], const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv) {
+  if constexpr (MODE == 2) mul_d2(x, y, pd, pd1, mv);
+  else mul<MODE == 1>(x, y, p, n0, mv);
 }
 
 // canonical form of a value in [0, p] (limbs as mul leaves them): carries rippled up through the
@@ -215,7 +286,7 @@ __device__ __forceinline__ void normalize(uint32_t (&x)[kLL], const uint32_t (&p
   (void)ln;
 }
 
-template <bool F>
+template <int MODE>
 __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, const uint8_t* __restrict__ base_be,
                                                   const uint8_t* __restrict__ exp_be, uint8_t* __restrict__ out_be,
                                                   uint32_t n) {
@@ -226,9 +297,15 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
   if (e >= n) return;
   const uint32_t ln = lane64();
   const uint32_t n0 = C->n0;
-  uint32_t p[kLL], x[kLL], y[kLL];
+  uint32_t mv;  // in a VGPR: v_and_b32_dpp takes its second operand from one
+  asm volatile("v_mov_b32 %0, %1" : "=v"(mv) : "s"(C->mask));
+  uint32_t p[kLL], x[kLL], y[kLL], pd[kLL], pd1[kLL];
 #pragma unroll
-  for (int j = 0; j < kLL; ++j) p[j] = C->p[kLL * ln + j];
+  for (int j = 0; j < kLL; ++j) {
+    p[j] = C->p[kLL * ln + j];
+    pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
+    pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
+  }
   // 512 big-endian bytes -> 128 little-endian words -> this lane's three limbs
   const uint32_t* be32 = reinterpret_cast<const uint32_t*>(base_be + (size_t)e * 512);
   for (uint32_t k = ln; k < 128; k += 64) s_w[127 - k] = __builtin_bswap32(be32[k]);
@@ -242,15 +319,15 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
     x[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & kM;
     y[j] = C->r2[kLL * ln + j];
   }
-  mul<F>(x, y, p, n0);  // Montgomery form (a base >= p is reduced here: x * R^2 * R^-1 < 2p)
+  mulm<MODE>(x, y, p, pd, pd1, n0, mv);  // Montgomery form (a base >= p is reduced here: x * R^2 * R^-1 < 2p)
   // odd powers for the 5-bit sliding window
   uint32_t x2[kLL] = {x[0], x[1], x[2]};
-  mul<F>(x2, x, p, n0);
+  mulm<MODE>(x2, x, p, pd, pd1, n0, mv);
 #pragma unroll
   for (int j = 0; j < kLL; ++j) s_tab[0][kLL * ln + j] = x[j];
 #pragma unroll 1
   for (int k = 1; k < 16; ++k) {
-    mul<F>(x, x2, p, n0);
+    mulm<MODE>(x, x2, p, pd, pd1, n0, mv);
 #pragma unroll
     for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = x[j];
   }
@@ -266,7 +343,7 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
     bool started = false;
     while (i >= 0) {
       if (!bit(i)) {
-        mul<F>(x, x, p, n0);
+        mulm<MODE>(x, x, p, pd, pd1, n0, mv);
         --i;
         continue;
       }
@@ -275,11 +352,11 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
       uint32_t val = 0;
       for (int k = i; k >= l; --k) val = val << 1 | bit(k);
       if (started)
-        for (int k = 0; k < i - l + 1; ++k) mul<F>(x, x, p, n0);
+        for (int k = 0; k < i - l + 1; ++k) mulm<MODE>(x, x, p, pd, pd1, n0, mv);
 #pragma unroll
       for (int j = 0; j < kLL; ++j) y[j] = s_tab[val >> 1][kLL * ln + j];
       if (started) {
-        mul<F>(x, y, p, n0);
+        mulm<MODE>(x, y, p, pd, pd1, n0, mv);
       } else {
 #pragma unroll
         for (int j = 0; j < kLL; ++j) x[j] = y[j];
@@ -291,7 +368,7 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
   // leave the Montgomery domain (x * 1 * R^-1: a value in [0, p]) and write canonical bytes
 #pragma unroll
   for (int j = 0; j < kLL; ++j) y[j] = (ln == 0 && j == 0) ? 1u : 0u;
-  mul<F>(x, y, p, n0);
+  mulm<MODE>(x, y, p, pd, pd1, n0, mv);
   normalize(x, p, ln);
   __syncthreads();
 #pragma unroll
@@ -309,6 +386,7 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
 
 struct PowWaveConsts {
   egw::Consts* d = nullptr;
+  bool d2 = false;  // p = -1 mod 2^58: the delayed-quotient multiply (EG_POWWAVE_D2=0 keeps mul<true>)
 };
 
 int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t* one, uint32_t n0, uint32_t friendly,
@@ -329,8 +407,32 @@ int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t*
   limbs(p, 128, h.p);
   limbs(r2, 129, h.r2);
   limbs(one, 129, h.one);
+  // p + 1 (129 words: the carry out of the top word is zero for p < 2^4096 - 1) in limbs, shifted down
+  // by two and by one limb for the delayed-quotient multiply
+  {
+    uint32_t p1[129];
+    uint64_t c = 1;
+    for (int k = 0; k < 128; ++k) {
+      c += p[k];
+      p1[k] = (uint32_t)c;
+      c >>= 32;
+    }
+    p1[128] = (uint32_t)c;
+    uint32_t pt[egw::kRow];
+    std::memset(pt, 0, sizeof pt);
+    limbs(p1, 129, pt);
+    for (int a = 0; a < egw::kRow; ++a) {
+      h.pd[a] = a + 2 < egw::kLimbs ? pt[a + 2] : 0u;
+      h.pd1[a] = a + 1 < egw::kLimbs ? pt[a + 1] : 0u;
+    }
+  }
   h.n0 = n0;
+  h.mask = egw::kM;
   auto* c = new PowWaveConsts();
+  {
+    const char* env = std::getenv("EG_POWWAVE_D2");
+    c->d2 = p[0] == 0xFFFFFFFFu && (p[1] & 0x03FFFFFFu) == 0x03FFFFFFu && !(env && env[0] == '0');
+  }
   hipError_t e = hipMalloc(&c->d, sizeof(egw::Consts));
   if (e == hipSuccess) e = hipMemcpy(c->d, &h, sizeof(egw::Consts), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -352,10 +454,12 @@ void powwave_consts_destroy(PowWaveConsts* c) {
 int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint8_t* base_be, const uint8_t* exp_be,
                  uint8_t* out_be, size_t n, std::string* err) {
   if (!n) return 0;
-  if (friendly)
-    hipLaunchKernelGGL(egw::k_powp_wave<true>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be, (uint32_t)n);
+  if (friendly && C->d2)
+    hipLaunchKernelGGL(egw::k_powp_wave<2>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be, (uint32_t)n);
+  else if (friendly)
+    hipLaunchKernelGGL(egw::k_powp_wave<1>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be, (uint32_t)n);
   else
-    hipLaunchKernelGGL(egw::k_powp_wave<false>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be,
+    hipLaunchKernelGGL(egw::k_powp_wave<0>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be,
                        (uint32_t)n);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

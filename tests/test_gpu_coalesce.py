@@ -50,7 +50,8 @@ def test_cpp_eleven_threads_per_element_bitexact(group, tmp_path):
 def test_latency_shape_for_blocking_callers(group, tmp_path):
     """The coalescer's small powP batches run on the latency-shaped layouts (eg_pow16.hip): one element
     per wave up to one per SIMD, 16-lane groups up to one resident round (EG_LATENCY_POW=16 skips the
-    per-wave one, =0 keeps every batch on the 8-lane layout).  Every layout is bit-exact on the edge
+    per-wave one, =0 keeps every batch on the 8-lane layout; EG_POWWAVE_D2=0 runs the per-wave kernel's
+    per-step-quotient multiply instead of the delayed-quotient one).  Every layout is bit-exact on the edge
     cases (bases 0, 1, p-1, p, p+1, 2^4096-1; exponents 0, 1, 2, q-1, q, 2^256-1).  One blocking
     caller gets its results at least twice as fast on the default as on the 8-lane layout, 11 blocking
     callers at least 1.6x (they also pay their own turn-around between batches; the window of the
@@ -69,7 +70,8 @@ def test_latency_shape_for_blocking_callers(group, tmp_path):
     vec = tmp_path / "vectors.bin"
     vec.write_bytes(struct.pack("<I", n) + b"".join(recs))
     res = {}
-    for shape, env in (("per-wave", {}), ("16-lane", {"EG_LATENCY_POW": "16"}), ("8-lane", {"EG_LATENCY_POW": "0"})):
+    for shape, env in (("per-wave", {}), ("per-wave-cios", {"EG_POWWAVE_D2": "0"}), ("16-lane", {"EG_LATENCY_POW": "16"}),
+                       ("8-lane", {"EG_LATENCY_POW": "0"})):
         for threads in (11, 1):
             r = subprocess.run([str(BIN), str(vec), str(threads)], capture_output=True, text=True, timeout=600,
                                env=dict(os.environ, **env))
@@ -83,6 +85,8 @@ def test_latency_shape_for_blocking_callers(group, tmp_path):
     assert res[("per-wave", 11)]["powp_one_blocking_per_s"] > 1.6 * res[("8-lane", 11)]["powp_one_blocking_per_s"]
     assert res[("per-wave", 1)]["powp_one_blocking_per_s"] > 2 * res[("8-lane", 1)]["powp_one_blocking_per_s"]
     assert res[("16-lane", 1)]["powp_one_blocking_per_s"] > 1.3 * res[("8-lane", 1)]["powp_one_blocking_per_s"]
+    # the delayed-quotient multiply (p = -1 mod 2^58) against the per-step quotient one
+    assert res[("per-wave", 1)]["powp_one_blocking_per_s"] > 1.1 * res[("per-wave-cios", 1)]["powp_one_blocking_per_s"]
 
 
 def test_python_threads_per_element_bitexact(group):

@@ -50,7 +50,7 @@ def main():
         vec1 = Path(d) / "v1.bin"
         vec1.write_bytes(struct.pack("<I", n1) + b"".join(recs[:n1]))
         res = {}
-        for shape, env in (("per-wave", {}), ("16-lane", {"EG_LATENCY_POW": "16"}),
+        for shape, env in (("per-wave", {}), ("per-wave-cios", {"EG_POWWAVE_D2": "0"}), ("16-lane", {"EG_LATENCY_POW": "16"}),
                            ("8-lane", {"EG_LATENCY_POW": "0"})):
             for threads in (11, 1):
                 r = subprocess.run([str(BIN), str(vec if threads > 1 else vec1), str(threads)], capture_output=True,
@@ -65,7 +65,7 @@ def main():
     out = {"n": a.n, "n_single_caller": min(a.n, a.n_single), "host_per_core_powp_per_s": a.per_core, "host_cores": a.cores,
            "host_11_threads_powp_per_s": cpu11, "host_all_cores_powp_per_s": cpu_all, "runs": res}
     # the batch size above which one GPU batch beats the host's cores on the same elements
-    for shape in ("per-wave", "16-lane", "8-lane"):
+    for shape in ("per-wave", "per-wave-cios", "16-lane", "8-lane"):
         sweep = res[f"{shape}/11"]["sweep"]
         out[f"crossover_vs_{a.cores}_cores_{shape}"] = next(
             (s["m"] for s in sweep if s["m"] / (s["coalesced_ms"] / 1e3) > cpu_all), None)
