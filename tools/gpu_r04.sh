@@ -54,4 +54,13 @@ if [[ $STEPS == *pipeg2* ]]; then
     --warmup 1 --modexp-n 0 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo2_pipeline.log 2>&1
   echo "pipeg2: $(tail -c 400 gpurun_out/${TAG}_rehearse_gloo2_pipeline.log)"
 fi
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1
+  echo "smoke: $(tail -n 1 gpurun_out/${TAG}_smoke.log)"
+fi
+if [[ $STEPS == *driver* ]]; then
+  # the driver's N = 1 command
+  timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench_driver_args.log 2>&1
+  echo "driver: $(tail -c 300 gpurun_out/${TAG}_bench_driver_args.log)"
+fi
 echo all done
