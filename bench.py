@@ -125,6 +125,12 @@ def exchange_mode() -> str:
     return "gloo" if m == "gloo" else "rccl"
 
 
+def note(rank, msg):
+    """Progress on stderr (rank 0; outside the timed region): stdout keeps the one JSON line."""
+    if rank == 0:
+        print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+
 def init_ranks(a):
     """-> (world, rank, device, dist): the host process group (gloo, CPU only) at N > 1."""
     from electionguard.launch import launched_world
@@ -236,10 +242,12 @@ def verify_tally(a, world, rank, local, dist):
         if not ok:
             raise RuntimeError("verification failed on honest synthetic ballots")
 
+    note(rank, f"setup done ({nb} ballots per rank resident); {a.warmup} warmup steps")
     for _ in range(a.warmup):
         step()
     if dist:
         dist.barrier()
+    note(rank, f"warmup done; {a.steps} timed steps")
     group.sync()
     group.profile_begin()
     t0 = time.perf_counter()
@@ -249,6 +257,7 @@ def verify_tally(a, world, rank, local, dist):
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    note(rank, f"timed steps done in {el:.2f} s")
     kp = group.profile_end()
     el = max_over_ranks(dist, el)
     xch.close()
@@ -597,10 +606,12 @@ def full_pipeline(a, world, rank, local, dist, keep=None):
             ph["exchange"] += t3 - t2
             ph["decrypt"] += t4 - t3
 
+    note(rank, f"setup done ({nb} ballots per rank); {a.warmup} warmup steps")
     for _ in range(a.warmup):
         step(False)
     if dist:
         dist.barrier()
+    note(rank, f"warmup done; {a.steps} timed steps")
     group.sync()
     group.profile_begin()
     t0 = time.perf_counter()
@@ -610,6 +621,7 @@ def full_pipeline(a, world, rank, local, dist, keep=None):
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    note(rank, f"timed steps done in {el:.2f} s")
     kp = group.profile_end()
     el = max_over_ranks(dist, el)
     phases = {k: max_over_ranks(dist, v) for k, v in ph.items()}
