@@ -711,7 +711,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     const std::string mode = lp ? lp : "";
     std::string err;
     if (mode != "0" && pow16_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->lat, &err) == 0)
-      c->lat_jobs = pow16_round_jobs(device);
+      c->lat_jobs = pow16_round_jobs(device) / 2;  // a full 16-lane round is slower than half an 8-lane one (r04l)
     if (mode != "0" && mode != "16" &&
         powwave_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->latw, &err) == 0) {
       int cus = 0;
@@ -919,10 +919,17 @@ static int pow_host(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, ui
   return EG_OK;
 }
 
+static bool latency_shaped(const eg_ctx* c, size_t n);  // eg_capi_coalesce.inc
+static int pow_latency(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n);
+
 extern "C" int eg_powp_batch(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n) {
   if (!c || (n && (!base_be || !exp_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
   if (!n) return EG_OK;
   Locked L(c);
+  // small batches on the latency layouts: up to one element per SIMD one element per wave (1.7-1.8
+  // against 3.7 ms on 8-lane groups), up to half a round 16-lane groups (3.2 against 3.8 ms at 4,096;
+  // profiles/r04m_coalesce_shapes.json)
+  if (latency_shaped(c, n)) return pow_latency(c, base_be, exp_be, out_be, n);
   return pow_host(c, base_be, exp_be, 32, false, out_be, n, nullptr);
 }
 

@@ -125,7 +125,9 @@ int eg_fixed_base_create(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], int win
                          eg_fixed_base** out);
 int eg_fixed_base_destroy(eg_fixed_base* fb);
 
-/* ElementModP.powP(ElementModQ), variable base: out[i] = base[i]^exp[i] mod p. */
+/* ElementModP.powP(ElementModQ), variable base: out[i] = base[i]^exp[i] mod p.  Up to one
+ * element per SIMD (1,024 on MI355X) runs one element per wave, up to half a resident round
+ * 16 lanes per element (latency shapes), larger batches on 8-lane groups. */
 int eg_powp_batch(eg_ctx* ctx, const uint8_t* base_be, const uint8_t* exp_be,
                   uint8_t* out_be, size_t n);
 /* Fixed-base powP (gPowP / accelerated K.powP): out[i] = base^exp[i] mod p. */
