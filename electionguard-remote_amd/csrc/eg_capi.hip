@@ -711,7 +711,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     const std::string mode = lp ? lp : "";
     std::string err;
     if (mode != "0" && pow16_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->lat, &err) == 0)
-      c->lat_jobs = pow16_round_jobs(device) / 2;  // a full 16-lane round is slower than half an 8-lane one (r04l)
+      c->lat_jobs = pow16_round_jobs(device) / 2;  // at 12,288 elements 16-lane groups ran 8.4 ms, 8-lane 7.3 (r04l)
     if (mode != "0" && mode != "16" &&
         powwave_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->latw, &err) == 0) {
       int cus = 0;

@@ -143,14 +143,15 @@ def test_profile_counts_and_clock(group):
     """eg_ctx_profile_end counts the k_pow work of the window from the op programs, and
     eg_ctx_profile_clock reports the shader clock it ran at (median per-workgroup s_memtime
     over s_memrealtime ticks, every record usable): a 4-bit-window powP is 14 table MMs +
-    63 x (4 sq + 1 mul).  Batches up to half a 16-lane round (6,144) run on the latency layouts
-    (eg_pow16.hip, not k_pow: nothing to count), so the counted batch is larger."""
+    63 x (4 sq + 1 mul).  Batches up to half a resident 16-lane round run on the latency layouts
+    (eg_pow16.hip, not k_pow: nothing to count), so the counted batch is larger (and within one
+    8-lane round: one launch)."""
     rng = np.random.default_rng(5)
     small = rng.integers(0, 256, size=(64, 512), dtype=np.uint8)
     group.profile_begin()
     group.powP_batch(small, rng.integers(0, 256, size=(64, 32), dtype=np.uint8))
     assert group.profile_end().launches == 0
-    n = 8192
+    n = 20000
     bases = rng.integers(0, 256, size=(n, 512), dtype=np.uint8)
     bases[:, 0] = 0
     exps = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
