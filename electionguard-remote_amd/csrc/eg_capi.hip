@@ -921,6 +921,7 @@ static int pow_host(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, ui
 
 static bool latency_shaped(const eg_ctx* c, size_t n);  // eg_capi_coalesce.inc
 static int pow_latency(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n);
+static int fb_latency(eg_ctx* c, const FbTab& t, const uint8_t* exp_be, uint8_t* out_be, size_t n);
 
 extern "C" int eg_powp_batch(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n) {
   if (!c || (n && (!base_be || !exp_be || !out_be))) return fail(EG_ERR_ARG, "null argument");
@@ -939,6 +940,7 @@ extern "C" int eg_fb_pow_batch(eg_fixed_base* fb, const uint8_t* exp_be, uint8_t
   eg_ctx* c = fb->ctx;
   Locked L(c);
   FbTab t = fb->tab();
+  if (c->latw && n <= c->latw_jobs) return fb_latency(c, t, exp_be, out_be, n);  // one element per wave
   return pow_host(c, nullptr, exp_be, 32, false, out_be, n, &t);
 }
 

@@ -41,3 +41,7 @@ void powwave_consts_destroy(PowWaveConsts* c);
 // out_be[i] = base_be[i]^exp_be[i] mod p (device pointers, asynchronous on s; no scratch)
 int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint8_t* base_be, const uint8_t* exp_be,
                  uint8_t* out_be, size_t n, std::string* err);
+// out_be[i] = base^exp_be[i] mod p over a fixed-base radix table (eg_fixed_base_create: (nwin << wbits)
+// 8-lane device elements in the Montgomery domain), one element per wave (device pointers, async on s)
+int powwave_fbpow(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint32_t* tab, uint32_t wbits,
+                  uint32_t nwin, const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err);

@@ -382,6 +382,77 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
     out32[b] = __builtin_bswap32((uint32_t)v);
   }
 }
+
+// Fixed-base powP on one wave per element: base^e = prod_k T[k][digit k of e] over the radix table
+// of eg_fixed_base_create (k_fb_level; entries in the Montgomery domain, 8-lane device element
+// format: limb i at word (i / 18) * 20 + i % 18), ceil(256 / w) - 1 multiplies instead of the
+// ~314 operations of a variable-base powP.  The digits are read by the whole wave (wave-uniform
+// loop; a zero digit skips its multiply, as the variable-time k_pow does).
+template <int MODE>
+__global__ void __launch_bounds__(64) k_fbpow_wave(const Consts* __restrict__ C, const uint32_t* __restrict__ tab,
+                                                   uint32_t wbits, uint32_t nwin, const uint8_t* __restrict__ exp_be,
+                                                   uint8_t* __restrict__ out_be, uint32_t n) {
+  __shared__ uint32_t s_w[kRow];  // limb -> byte staging
+  __shared__ uint32_t s_e[9];     // the exponent, little-endian words, and a zero word above it
+  const uint32_t e = blockIdx.x;  // one element per workgroup of one wave; the grid is exactly n
+  if (e >= n) return;
+  const uint32_t ln = lane64();
+  const uint32_t n0 = C->n0;
+  uint32_t mv;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(mv) : "s"(C->mask));
+  uint32_t p[kLL], x[kLL], y[kLL], pd[kLL], pd1[kLL];
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) {
+    p[j] = C->p[kLL * ln + j];
+    pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
+    pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
+  }
+  if (ln < 8) s_e[7 - ln] = __builtin_bswap32(reinterpret_cast<const uint32_t*>(exp_be + (size_t)e * 32)[ln]);
+  if (ln == 8) s_e[8] = 0u;
+  __syncthreads();
+  const uint32_t dmask = (1u << wbits) - 1u;
+  bool started = false;
+#pragma unroll 1
+  for (uint32_t k = 0; k < nwin; ++k) {
+    const uint32_t bit = k * wbits, wi = bit >> 5;  // bit < 256: wi + 1 <= 8
+    const uint64_t v = ((uint64_t)__builtin_amdgcn_readfirstlane(s_e[wi + 1]) << 32) |
+                       __builtin_amdgcn_readfirstlane(s_e[wi]);
+    const uint32_t d = (uint32_t)(v >> (bit & 31)) & dmask;
+    if (d == 0) continue;
+    const uint32_t* ent = tab + ((size_t)(k << wbits) + d) * 160;
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) {
+      const uint32_t i = kLL * ln + j;
+      y[j] = ln < (uint32_t)kLanes ? ent[(i / 18) * 20 + i % 18] : 0u;
+    }
+    if (started) {
+      mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) x[j] = y[j];
+      started = true;
+    }
+  }
+  if (!started) {
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];  // e = 0: 1
+  }
+  // leave the Montgomery domain and write canonical bytes (as k_powp_wave)
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) y[j] = (ln == 0 && j == 0) ? 1u : 0u;
+  mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+  normalize(x, p, ln);
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) s_w[kLL * ln + j] = x[j];
+  __syncthreads();
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out_be + (size_t)e * 512);
+  for (uint32_t b = ln; b < 128; b += 64) {
+    const int bitpos = 32 * (127 - (int)b), a = bitpos / kBits, sh = bitpos - a * kBits;
+    auto limb = [&](int k) -> uint64_t { return k < kLimbs ? (uint64_t)s_w[k] : 0ull; };
+    const uint64_t val = (limb(a) >> sh) | (limb(a + 1) << (kBits - sh)) | (limb(a + 2) << (2 * kBits - sh));
+    out32[b] = __builtin_bswap32((uint32_t)val);
+  }
+}
 }  // namespace egw
 
 struct PowWaveConsts {
@@ -464,6 +535,30 @@ int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uin
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     *err = std::string("powwave launch: ") + hipGetErrorString(e);
+    return 1;
+  }
+  return 0;
+}
+
+int powwave_fbpow(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint32_t* tab, uint32_t wbits,
+                  uint32_t nwin, const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
+  if (!n) return 0;
+  if (wbits < 1 || wbits > 24 || (uint64_t)nwin * wbits < 256 || (uint64_t)(nwin - 1) * wbits >= 256) {
+    *err = "powwave fbpow: table shape";
+    return 1;
+  }
+  if (friendly && C->d2)
+    hipLaunchKernelGGL(egw::k_fbpow_wave<2>, dim3((unsigned)n), dim3(64), 0, s, C->d, tab, wbits, nwin, exp_be, out_be,
+                       (uint32_t)n);
+  else if (friendly)
+    hipLaunchKernelGGL(egw::k_fbpow_wave<1>, dim3((unsigned)n), dim3(64), 0, s, C->d, tab, wbits, nwin, exp_be, out_be,
+                       (uint32_t)n);
+  else
+    hipLaunchKernelGGL(egw::k_fbpow_wave<0>, dim3((unsigned)n), dim3(64), 0, s, C->d, tab, wbits, nwin, exp_be, out_be,
+                       (uint32_t)n);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    *err = std::string("powwave fbpow launch: ") + hipGetErrorString(e);
     return 1;
   }
   return 0;
