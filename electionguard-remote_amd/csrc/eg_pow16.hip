@@ -415,8 +415,9 @@ __global__ void __launch_bounds__(64) k_fbpow_wave(const Consts* __restrict__ C,
 #pragma unroll 1
   for (uint32_t k = 0; k < nwin; ++k) {
     const uint32_t bit = k * wbits, wi = bit >> 5;  // bit < 256: wi + 1 <= 8
-    const uint64_t v = ((uint64_t)__builtin_amdgcn_readfirstlane(s_e[wi + 1]) << 32) |
-                       __builtin_amdgcn_readfirstlane(s_e[wi]);
+    // (readfirstlane returns int: widen through uint32_t, not with sign extension)
+    const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_e[wi + 1]) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_e[wi]);
     const uint32_t d = (uint32_t)(v >> (bit & 31)) & dmask;
     if (d == 0) continue;
     const uint32_t* ent = tab + ((size_t)(k << wbits) + d) * 160;
