@@ -260,11 +260,13 @@ def verify_tally(a, world, rank, local, dist):
     note(rank, f"timed steps done in {el:.2f} s")
     kp = group.profile_end()
     el = max_over_ranks(dist, el)
+    rccl_ranks = xch.rccl_ranks  # what RCCL itself reports (ncclCommCount), before the communicator closes
     xch.close()
 
     value = nb * world * a.steps / el
     out = line_common(a, world, el, value, kp, nb, man, "ballots verified+tallied/sec (node, 4096-bit group)",
                       xch.collective)
+    out["config"]["rccl_ranks"] = rccl_ranks
     if xch.note:
         out["config"]["exchange_note"] = xch.note
     out["modexp_per_s_per_gpu"] = {"var_base": modexp.get("var_base_per_s"),
@@ -328,7 +330,8 @@ def line_common(a, world, el, value, kp, nb, man, metric, collective):
             "ballots_per_gpu": nb,
             "selections_per_ballot": man.nsel,
             "fb_window_bits": a.fb_window,
-            "parallelism": f"ballot-sharded x{world}, {collective} all-gather of partial tallies",
+            "parallelism": (f"ballot-sharded x{world}, {collective} all-gather of partial tallies" if world > 1 else
+                            f"ballot-sharded x1, {collective}"),
         },
         "roofline": {
             "bound": "valu-int",
@@ -625,11 +628,13 @@ def full_pipeline(a, world, rank, local, dist, keep=None):
     kp = group.profile_end()
     el = max_over_ranks(dist, el)
     phases = {k: max_over_ranks(dist, v) for k, v in ph.items()}
+    rccl_ranks = xch.rccl_ranks
     xch.close()
     value = nb * world * a.steps / el
     out = line_common(a, world, el, value, kp, nb, man,
                       "ballots encrypted+verified+tallied+decrypted/sec (node, 4096-bit group, full pipeline)",
                       xch.collective)
+    out["config"]["rccl_ranks"] = rccl_ranks
     if xch.note:
         out["config"]["exchange_note"] = xch.note
     tot = nb * world * a.steps

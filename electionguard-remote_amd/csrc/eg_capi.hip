@@ -140,6 +140,10 @@ struct eg_fixed_base {
   eg_ctx* ctx = nullptr;
   uint32_t* d_tab = nullptr;
   int wbits = 0, nwin = 0;
+  std::array<uint8_t, 512> base{};  // the base (big-endian), for the constant-time companion table
+  // constant-time companion (eg_ctx_set_ct_pow): the same base at a window a masked scan can read
+  // (kCtEncWindow bits), built on first constant-time use when wbits > kCtMaxWindow; owned
+  eg_fixed_base* ct = nullptr;
   FbTab tab() const { return FbTab{d_tab, (uint32_t)wbits, (uint32_t)nwin}; }
 };
 
@@ -190,6 +194,7 @@ struct eg_ctx {
   std::map<std::string, SchedBuf> sched;  // k_pow op programs per launch shape (pow_schedule_dev)
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
   uint32_t ct_encrypt = 0;              // encryption on k_pow<F, true> with small CT tables (eg_ctx_set_ct_encrypt)
+  uint32_t ct_pow = 0;                  // powP / fixed-base / per-element calls constant-time (eg_ctx_set_ct_pow)
   int ct_window = kCtEncWindow;         // their radix width
   eg_fixed_base* g_ct = nullptr;  // g's kCtEncWindow-bit table (K's live in keys[].ct)
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
@@ -220,6 +225,9 @@ struct eg_ctx {
   size_t lat_jobs = 0;
   PowWaveConsts* latw = nullptr;
   size_t latw_jobs = 0;
+  // the coalescer runs a batch of up to wave_max jobs on the per-wave kernel (any mix of kinds);
+  // larger batches of one plain kind keep the throughput layouts (EG_WAVE_MAX overrides)
+  size_t wave_max = 0;
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
 
@@ -475,10 +483,10 @@ static int launch_pow(eg_ctx* c, const PowShape& S, const uint32_t* d_jobs, size
   if (tail2 && !tail) std::swap(tail, tail2);
   if (scratch && (tail || njobs > kPowMaxJobs || njobs > kGroupsPerBlock))
     return fail(EG_ERR_ARG, "an explicit k_pow scratch takes one workgroup of jobs and no tail");
-  // constant-time shapes: a comb (masked scans of its tables) without fixed-base terms, or
-  // fixed-base terms alone from small-window tables (masked scans of 2^w-entry window columns)
+  // constant-time shapes: a comb or a 4-bit window (masked scans of their tables) without fixed-base
+  // terms, or fixed-base terms alone from small-window tables (masked scans of 2^w-entry window columns)
   auto ct_shape = [&](const PowShape& X) {
-    if (X.has_base) return X.comb && !X.gather && !X.nfb[0] && !X.nfb[1];
+    if (X.has_base) return !X.gather && !X.nfb[0] && !X.nfb[1];  // a comb or a 4-bit window
     return f0.wbits <= kCtMaxWindow && f1.wbits <= kCtMaxWindow;
   };
   // every population of the launch: its shape and the buffers it needs
@@ -659,6 +667,7 @@ static int fb_create_locked(eg_ctx* c, const uint8_t base_be[512], int wbits, eg
   if (rc) return rc;
   auto* fb = new eg_fixed_base();
   fb->ctx = c;
+  std::memcpy(fb->base.data(), base_be, 512);
   rc = build_fb(c, d_m, wbits, fb);
   hipFree(d_m);
   if (rc) {
@@ -717,6 +726,8 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
       int cus = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
         c->latw_jobs = (size_t)cus * 4;  // one element per SIMD
+      c->wave_max = c->latw_jobs;
+      if (const char* wm = getenv("EG_WAVE_MAX")) c->wave_max = (size_t)std::max(0L, atol(wm));
     }
   }
   {  // c = 2^256 - q (mod 2^256) for the residue test x^(2^256) == x^c
@@ -776,7 +787,23 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
 extern "C" int eg_fixed_base_destroy(eg_fixed_base* fb) {
   if (!fb) return EG_OK;
   if (fb->d_tab) hipFree(fb->d_tab);
+  eg_fixed_base_destroy(fb->ct);
   delete fb;
+  return EG_OK;
+}
+
+// The table a constant-time read of fb's base uses: fb itself when a masked scan of its window
+// columns is affordable (wbits <= kCtMaxWindow), else its kCtEncWindow-bit companion, built once.
+static int ct_table_locked(eg_ctx* c, eg_fixed_base* fb, FbTab* out) {
+  if (fb->wbits <= (int)kCtMaxWindow) {
+    *out = fb->tab();
+    return EG_OK;
+  }
+  if (!fb->ct) {
+    const int rc = fb_create_locked(c, fb->base.data(), kCtEncWindow, &fb->ct);
+    if (rc) return rc;
+  }
+  *out = fb->ct->tab();
   return EG_OK;
 }
 
@@ -911,7 +938,10 @@ static int pow_host(eg_ctx* c, const uint8_t* base_be, const uint8_t* exp_be, ui
   if ((rc = upload(c, W_JOBS, jobs.data(), jobs.size() * 4, (void**)&d_jobs))) return rc;
   if ((rc = ws_get(c, W_E1, n * kW * 4, (void**)&d_o))) return rc;
   FbTab f0 = fbonly ? *fbonly : c->gtab->tab();
-  if ((rc = launch_pow(c, S, d_jobs, n, d_e, d_exp, d_o, f0, f0))) return rc;
+  // eg_ctx_set_ct_pow: the window / fixed-base schedule of k_pow<F, true> (a public exponent, the
+  // inverse's p - 2, keeps the variable-time instantiation)
+  const bool ct = c->ct_pow && exp_bytes == 32;
+  if ((rc = launch_pow(c, S, d_jobs, n, d_e, d_exp, d_o, f0, f0, nullptr, nullptr, nullptr, nullptr, ct))) return rc;
   if ((rc = ws_get(c, W_OUT, n * 512, (void**)&d_out))) return rc;
   if ((rc = launch_export(c, d_o, n, d_out))) return rc;
   HIPCHK(hipMemcpyAsync(out_be, d_out, n * 512, hipMemcpyDeviceToHost, c->stream));
@@ -940,6 +970,10 @@ extern "C" int eg_fb_pow_batch(eg_fixed_base* fb, const uint8_t* exp_be, uint8_t
   eg_ctx* c = fb->ctx;
   Locked L(c);
   FbTab t = fb->tab();
+  if (c->ct_pow) {
+    const int rc = ct_table_locked(c, fb, &t);
+    if (rc) return rc;
+  }
   if (c->latw && n <= c->latw_jobs) return fb_latency(c, t, exp_be, out_be, n);  // one element per wave
   return pow_host(c, nullptr, exp_be, 32, false, out_be, n, &t);
 }
@@ -1167,7 +1201,8 @@ static int pow_dev(eg_ctx* c, const uint8_t* d_base_be, const uint8_t* d_exp_be,
   }
   if ((rc = ws_get(c, W_E1, n * kW * 4, (void**)&d_o))) return rc;
   FbTab f0 = fbonly ? *fbonly : c->gtab->tab();
-  if ((rc = launch_pow(c, S, d_jobs, n, d_e, d_exp_be, d_o, f0, f0))) return rc;
+  if ((rc = launch_pow(c, S, d_jobs, n, d_e, d_exp_be, d_o, f0, f0, nullptr, nullptr, nullptr, nullptr, c->ct_pow != 0)))
+    return rc;
   return launch_export(c, d_o, n, d_out_be);
 }
 
@@ -1185,5 +1220,9 @@ extern "C" int eg_fb_pow_batch_dev(eg_fixed_base* fb, const uint8_t* d_exp_be, u
   eg_ctx* c = fb->ctx;
   Locked L(c);
   FbTab t = fb->tab();
+  if (c->ct_pow) {
+    const int rc = ct_table_locked(c, fb, &t);
+    if (rc) return rc;
+  }
   return pow_dev(c, nullptr, d_exp_be, d_out_be, n, &t);
 }

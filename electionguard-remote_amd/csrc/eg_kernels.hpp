@@ -519,10 +519,12 @@ struct PowPart {
 
 // CT = true: the constant-time instantiation for secret exponents (trustee shares s_i and
 // P_l(x_i), proof nonces u; encryption nonces R, u and the vote with eg_ctx_set_ct_encrypt).
-// Comb shapes and small-window radix fixed-base terms (no 4-bit window): every comb-table read
-// is ct_select_to_lds over the block's whole table, every fixed-base read over the window's
-// whole column, and the square/multiply schedule is fixed by the shape, so neither time nor
-// addresses depend on exponent bits.
+// Comb shapes, 4-bit window shapes (variable-base powP with eg_ctx_set_ct_pow: the window
+// schedule is fixed, 4 squarings + 1 multiply per nibble, a zero nibble multiplies by tbl[0] = 1)
+// and small-window radix fixed-base terms: every comb- or window-table read is ct_select_to_lds
+// over the block's whole table, every fixed-base read over the window's whole column, and the
+// square/multiply schedule is fixed by the shape, so neither time nor addresses depend on
+// exponent bits.
 template <bool F, bool CT>
 __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* __restrict__ C, PowPart P0,
                                                 PowPart P1, PowPart P2, const uint32_t* __restrict__ elems,
@@ -589,7 +591,18 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
           case OP_LOAD_ONE: load_elem(x, C->one); break;
           case OP_LOAD_BASE: load_elem(x, B); break;
           case OP_LOAD_TBL: load_elem(x, tbl + (size_t)arg * kW); break;
-          case OP_LOAD_WIN: load_elem(x, tbl + (size_t)(scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4) * kW); break;
+          case OP_LOAD_WIN: {
+            const uint32_t d = scalars[(size_t)J[1 + arg] * S.exp_bytes] >> 4;
+            if constexpr (CT) {  // secret exponent (eg_ctx_set_ct_pow): masked scan of the 16-entry table
+              ct_select_to_lds(slot, tbl, 4, d);
+              wave_sync();
+              load_elem(x, slot);
+              wave_sync();
+            } else {
+              load_elem(x, tbl + (size_t)d * kW);
+            }
+            break;
+          }
           case OP_LOAD_COMB:
             if constexpr (CT) {
               ct_select_to_lds(slot, tbl, ch, dig[arg]);
@@ -650,6 +663,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       const uint32_t w = arg & 4095u;
       const uint32_t byte = scalars[(size_t)J[1 + (arg >> 12)] * S.exp_bytes + (w >> 1)];
       ysrc = tbl + (size_t)((w & 1) ? (byte & 15u) : (byte >> 4)) * kW;
+      fb_d = (w & 1) ? (byte & 15u) : (byte >> 4);  // CT: the window digit the masked scan selects
     } else if (kind == OP_MUL_COMB) ysrc = tbl + (size_t)dig[arg] * kW;
     else if (kind == OP_MUL_GATHER) ysrc = P.ygat + ((size_t)(J[2] + (arg >> 2)) * (kCombH - 1) + (arg & 3u)) * kW;
     else if (kind == OP_MUL_FB) {
@@ -667,6 +681,7 @@ __global__ void __launch_bounds__(kBlock, EG_MIN_WAVES) k_pow(const MontConsts* 
       if constexpr (CT) {
         if (kind == OP_MUL_COMB) ct_select_to_lds(slot, tbl, ch, dig[arg]);  // secret digit
         else if (kind == OP_MUL_FB) ct_select_to_lds(slot, fb_col, fb_h, fb_d);
+        else if (kind == OP_MUL_WIN) ct_select_to_lds(slot, tbl, 4, fb_d);  // secret nibble
         else elem_to_lds(slot, ysrc);
       } else {
         elem_to_lds(slot, ysrc);

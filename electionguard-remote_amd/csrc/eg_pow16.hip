@@ -83,7 +83,7 @@ size_t pow16_round_jobs(int device) {
   return (size_t)cus * (size_t)per_cu * kGroupsPerBlock;
 }
 
-int pow16_powp(const Pow16Consts* C, bool friendly, hipStream_t s, const uint32_t* sched, const uint32_t* jobs,
+int pow16_powp(const Pow16Consts* C, bool friendly, bool ct, hipStream_t s, const uint32_t* sched, const uint32_t* jobs,
                const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n, uint32_t* elems,
                uint32_t* outs, uint32_t* scratch, std::string* err) {
   if (!n) return 0;
@@ -97,13 +97,21 @@ int pow16_powp(const Pow16Consts* C, bool friendly, hipStream_t s, const uint32_
   const FbTab nofb{nullptr, 0, 0};
   if (friendly) {
     hipLaunchKernelGGL(k_import<true>, dim3(grid), dim3(kBlock), 0, s, C->d, base_be, (uint32_t)n, elems, nullptr);
-    hipLaunchKernelGGL((k_pow<true, false>), dim3(grid), dim3(kBlock), 0, s, C->d, P0, none, none, elems, exp_be, outs,
-                       nofb, nofb, nullptr);
+    if (ct)
+      hipLaunchKernelGGL((k_pow<true, true>), dim3(grid), dim3(kBlock), 0, s, C->d, P0, none, none, elems, exp_be, outs,
+                         nofb, nofb, nullptr);
+    else
+      hipLaunchKernelGGL((k_pow<true, false>), dim3(grid), dim3(kBlock), 0, s, C->d, P0, none, none, elems, exp_be, outs,
+                         nofb, nofb, nullptr);
     hipLaunchKernelGGL(k_export<true>, dim3(grid), dim3(kBlock), 0, s, C->d, outs, (uint32_t)n, out_be);
   } else {
     hipLaunchKernelGGL(k_import<false>, dim3(grid), dim3(kBlock), 0, s, C->d, base_be, (uint32_t)n, elems, nullptr);
-    hipLaunchKernelGGL((k_pow<false, false>), dim3(grid), dim3(kBlock), 0, s, C->d, P0, none, none, elems, exp_be,
-                       outs, nofb, nofb, nullptr);
+    if (ct)
+      hipLaunchKernelGGL((k_pow<false, true>), dim3(grid), dim3(kBlock), 0, s, C->d, P0, none, none, elems, exp_be,
+                         outs, nofb, nofb, nullptr);
+    else
+      hipLaunchKernelGGL((k_pow<false, false>), dim3(grid), dim3(kBlock), 0, s, C->d, P0, none, none, elems, exp_be,
+                         outs, nofb, nofb, nullptr);
     hipLaunchKernelGGL(k_export<false>, dim3(grid), dim3(kBlock), 0, s, C->d, outs, (uint32_t)n, out_be);
   }
   const hipError_t e = hipGetLastError();
@@ -286,30 +294,11 @@ __device__ __forceinline__ void normalize(uint32_t (&x)[kLL], const uint32_t (&p
   (void)ln;
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, const uint8_t* __restrict__ base_be,
-                                                  const uint8_t* __restrict__ exp_be, uint8_t* __restrict__ out_be,
-                                                  uint32_t n) {
-  __shared__ uint32_t s_tab[16][kRow];  // x^1, x^3, ..., x^31 (Montgomery form)
-  __shared__ uint32_t s_w[kRow];        // byte <-> limb staging
-  __shared__ uint32_t s_e[8];           // the exponent, little-endian words
-  const uint32_t e = blockIdx.x;       // one element per workgroup of one wave; the grid is exactly n
-  if (e >= n) return;
-  const uint32_t ln = lane64();
-  const uint32_t n0 = C->n0;
-  uint32_t mv;  // in a VGPR: v_and_b32_dpp takes its second operand from one
-  asm volatile("v_mov_b32 %0, %1" : "=v"(mv) : "s"(C->mask));
-  uint32_t p[kLL], x[kLL], y[kLL], pd[kLL], pd1[kLL];
-#pragma unroll
-  for (int j = 0; j < kLL; ++j) {
-    p[j] = C->p[kLL * ln + j];
-    pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
-    pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
-  }
-  // 512 big-endian bytes -> 128 little-endian words -> this lane's three limbs
-  const uint32_t* be32 = reinterpret_cast<const uint32_t*>(base_be + (size_t)e * 512);
+// 512 big-endian bytes -> this lane's three limbs, staged through s_w (the whole wave takes part)
+__device__ __forceinline__ void import_be(const uint8_t* __restrict__ be, uint32_t (&x)[kLL], uint32_t* s_w, uint32_t ln) {
+  const uint32_t* be32 = reinterpret_cast<const uint32_t*>(be);
+  __syncthreads();  // s_w may still be read by the previous import
   for (uint32_t k = ln; k < 128; k += 64) s_w[127 - k] = __builtin_bswap32(be32[k]);
-  if (ln < 8) s_e[7 - ln] = __builtin_bswap32(reinterpret_cast<const uint32_t*>(exp_be + (size_t)e * 32)[ln]);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kLL; ++j) {
@@ -317,29 +306,100 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
     const uint32_t lo = (ln < kLanes && wi < 128) ? s_w[wi] : 0u;
     const uint32_t hi = (ln < kLanes && wi + 1 < 128) ? s_w[wi + 1] : 0u;
     x[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & kM;
-    y[j] = C->r2[kLL * ln + j];
   }
-  mulm<MODE>(x, y, p, pd, pd1, n0, mv);  // Montgomery form (a base >= p is reduced here: x * R^2 * R^-1 < 2p)
-  // odd powers for the 5-bit sliding window
-  uint32_t x2[kLL] = {x[0], x[1], x[2]};
-  mulm<MODE>(x2, x, p, pd, pd1, n0, mv);
-#pragma unroll
-  for (int j = 0; j < kLL; ++j) s_tab[0][kLL * ln + j] = x[j];
-#pragma unroll 1
-  for (int k = 1; k < 16; ++k) {
-    mulm<MODE>(x, x2, p, pd, pd1, n0, mv);
-#pragma unroll
-    for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = x[j];
-  }
+}
+
+// canonical limbs (normalize) -> 512 big-endian bytes
+__device__ __forceinline__ void export_be(const uint32_t (&x)[kLL], uint8_t* __restrict__ out_be, uint32_t* s_w,
+                                          uint32_t ln) {
   __syncthreads();
-  // the exponent, read by the whole wave (readfirstlane: every branch below is wave-uniform)
-  auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_e[i >> 5]) >> (i & 31)) & 1u; };
-  int i = 255;
-  while (i >= 0 && !bit(i)) --i;
-  if (i < 0) {
 #pragma unroll
-    for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];  // x^0 = 1 (also 0^0)
+  for (int j = 0; j < kLL; ++j) s_w[kLL * ln + j] = x[j];
+  __syncthreads();
+  uint32_t* out32 = reinterpret_cast<uint32_t*>(out_be);
+  for (uint32_t b = ln; b < 128; b += 64) {  // big-endian word b = little-endian word 127 - b
+    const int bitpos = 32 * (127 - (int)b), a = bitpos / kBits, sh = bitpos - a * kBits;
+    auto limb = [&](int k) -> uint64_t { return k < kLimbs ? (uint64_t)s_w[k] : 0ull; };
+    const uint64_t v = (limb(a) >> sh) | (limb(a + 1) << (kBits - sh)) | (limb(a + 2) << (2 * kBits - sh));
+    out32[b] = __builtin_bswap32((uint32_t)v);
+  }
+}
+
+// wave-uniform read of bits [bit, bit + w) of a little-endian exponent staged in LDS (9 words, the
+// last one zero, so a window that runs past bit 255 reads zeros)
+__device__ __forceinline__ uint32_t exp_digit(const uint32_t* s_x, uint32_t bit, uint32_t w) {
+  const uint32_t wi = bit >> 5;
+  // (readfirstlane returns int: widen through uint32_t, not with sign extension)
+  const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_x[wi + 1]) << 32) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_x[wi]);
+  return (uint32_t)(v >> (bit & 31)) & ((1u << w) - 1u);
+}
+
+// x <- x^e for the exponent staged in s_x (256 bits).  Variable time: a 5-bit sliding window
+// over the odd powers x^1, x^3, ..., x^31 (16 LDS entries, ~314 Montgomery operations for a random
+// 256-bit exponent, every branch wave-uniform).  Constant time (CT): x^0 .. x^15 in LDS and a fixed
+// 4-bit window, 14 + 63 x (4 squarings + 1 multiply) operations for every exponent, every table
+// read a masked scan of all 16 entries (neither the schedule nor an address depends on e).
+template <int MODE, bool CT>
+__device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x, uint32_t (*s_tab)[kRow],
+                                        const Consts* __restrict__ C, const uint32_t (&p)[kLL],
+                                        const uint32_t (&pd)[kLL], const uint32_t (&pd1)[kLL], uint32_t n0,
+                                        uint32_t mv, uint32_t ln) {
+  uint32_t y[kLL];
+  if constexpr (CT) {
+    __syncthreads();  // s_tab may still be read by a previous exponentiation
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) {
+      s_tab[0][kLL * ln + j] = C->one[kLL * ln + j];
+      s_tab[1][kLL * ln + j] = x[j];
+      y[j] = x[j];
+    }
+#pragma unroll 1
+    for (int k = 2; k < 16; ++k) {
+      mulm<MODE>(y, x, p, pd, pd1, n0, mv);
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = y[j];
+    }
+    __syncthreads();
+    auto select = [&](uint32_t (&dst)[kLL], uint32_t d) {
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) dst[j] = 0u;
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t m = 0u - (uint32_t)(k == d);
+#pragma unroll
+        for (int j = 0; j < kLL; ++j) dst[j] |= s_tab[k][kLL * ln + j] & m;
+      }
+    };
+    select(x, exp_digit(s_x, 252, 4));
+#pragma unroll 1
+    for (int w = 62; w >= 0; --w) {
+#pragma unroll 1
+      for (int s = 0; s < 4; ++s) mulm<MODE>(x, x, p, pd, pd1, n0, mv);
+      select(y, exp_digit(s_x, (uint32_t)(4 * w), 4));
+      mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+    }
   } else {
+    uint32_t x2[kLL] = {x[0], x[1], x[2]};
+    mulm<MODE>(x2, x, p, pd, pd1, n0, mv);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) s_tab[0][kLL * ln + j] = x[j];
+#pragma unroll 1
+    for (int k = 1; k < 16; ++k) {
+      mulm<MODE>(x, x2, p, pd, pd1, n0, mv);
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = x[j];
+    }
+    __syncthreads();
+    auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_x[i >> 5]) >> (i & 31)) & 1u; };
+    int i = 255;
+    while (i >= 0 && !bit(i)) --i;
+    if (i < 0) {
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];  // x^0 = 1 (also 0^0)
+      return;
+    }
     bool started = false;
     while (i >= 0) {
       if (!bit(i)) {
@@ -365,66 +425,44 @@ __global__ void __launch_bounds__(64) k_powp_wave(const Consts* __restrict__ C, 
       i = l - 1;
     }
   }
-  // leave the Montgomery domain (x * 1 * R^-1: a value in [0, p]) and write canonical bytes
-#pragma unroll
-  for (int j = 0; j < kLL; ++j) y[j] = (ln == 0 && j == 0) ? 1u : 0u;
-  mulm<MODE>(x, y, p, pd, pd1, n0, mv);
-  normalize(x, p, ln);
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kLL; ++j) s_w[kLL * ln + j] = x[j];
-  __syncthreads();
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out_be + (size_t)e * 512);
-  for (uint32_t b = ln; b < 128; b += 64) {  // big-endian word b = little-endian word 127 - b
-    const int bitpos = 32 * (127 - (int)b), a = bitpos / kBits, sh = bitpos - a * kBits;
-    auto limb = [&](int k) -> uint64_t { return k < kLimbs ? (uint64_t)s_w[k] : 0ull; };
-    const uint64_t v = (limb(a) >> sh) | (limb(a + 1) << (kBits - sh)) | (limb(a + 2) << (2 * kBits - sh));
-    out32[b] = __builtin_bswap32((uint32_t)v);
-  }
 }
 
-// Fixed-base powP on one wave per element: base^e = prod_k T[k][digit k of e] over the radix table
-// of eg_fixed_base_create (k_fb_level; entries in the Montgomery domain, 8-lane device element
-// format: limb i at word (i / 18) * 20 + i % 18), ceil(256 / w) - 1 multiplies instead of the
-// ~314 operations of a variable-base powP.  The digits are read by the whole wave (wave-uniform
-// loop; a zero digit skips its multiply, as the variable-time k_pow does).
-template <int MODE>
-__global__ void __launch_bounds__(64) k_fbpow_wave(const Consts* __restrict__ C, const uint32_t* __restrict__ tab,
-                                                   uint32_t wbits, uint32_t nwin, const uint8_t* __restrict__ exp_be,
-                                                   uint8_t* __restrict__ out_be, uint32_t n) {
-  __shared__ uint32_t s_w[kRow];  // limb -> byte staging
-  __shared__ uint32_t s_e[9];     // the exponent, little-endian words, and a zero word above it
-  const uint32_t e = blockIdx.x;  // one element per workgroup of one wave; the grid is exactly n
-  if (e >= n) return;
-  const uint32_t ln = lane64();
-  const uint32_t n0 = C->n0;
-  uint32_t mv;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(mv) : "s"(C->mask));
-  uint32_t p[kLL], x[kLL], y[kLL], pd[kLL], pd1[kLL];
+// x <- x * T^e (or x <- T^e when !started) over a fixed-base radix table (eg_fixed_base_create: entries
+// in the Montgomery domain, 8-lane element layout, limb i at word (i / 18) * 20 + i % 18 of a 160-word
+// entry): one multiply per window.  Variable time: a zero digit skips its window.  CT: every window is
+// multiplied in, its entry a masked scan of the window's whole column (tables of <= 8 bits only).
+template <int MODE, bool CT>
+__device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, const WaveTab& T, const uint32_t* s_x,
+                                          const uint32_t (&p)[kLL], const uint32_t (&pd)[kLL],
+                                          const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv, uint32_t ln) {
+  uint32_t y[kLL];
+  uint32_t idx[kLL];
 #pragma unroll
   for (int j = 0; j < kLL; ++j) {
-    p[j] = C->p[kLL * ln + j];
-    pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
-    pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
+    const uint32_t i = kLL * ln + j;
+    idx[j] = (i / 18) * 20 + i % 18;
   }
-  if (ln < 8) s_e[7 - ln] = __builtin_bswap32(reinterpret_cast<const uint32_t*>(exp_be + (size_t)e * 32)[ln]);
-  if (ln == 8) s_e[8] = 0u;
-  __syncthreads();
-  const uint32_t dmask = (1u << wbits) - 1u;
-  bool started = false;
+  const bool live = ln < (uint32_t)kLanes;
 #pragma unroll 1
-  for (uint32_t k = 0; k < nwin; ++k) {
-    const uint32_t bit = k * wbits, wi = bit >> 5;  // bit < 256: wi + 1 <= 8
-    // (readfirstlane returns int: widen through uint32_t, not with sign extension)
-    const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_e[wi + 1]) << 32) |
-                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(s_e[wi]);
-    const uint32_t d = (uint32_t)(v >> (bit & 31)) & dmask;
-    if (d == 0) continue;
-    const uint32_t* ent = tab + ((size_t)(k << wbits) + d) * 160;
+  for (uint32_t k = 0; k < T.nwin; ++k) {
+    const uint32_t d = exp_digit(s_x, k * T.wbits, T.wbits);
+    const uint32_t* col = T.data + ((size_t)k << T.wbits) * 160;
+    if constexpr (CT) {
 #pragma unroll
-    for (int j = 0; j < kLL; ++j) {
-      const uint32_t i = kLL * ln + j;
-      y[j] = ln < (uint32_t)kLanes ? ent[(i / 18) * 20 + i % 18] : 0u;
+      for (int j = 0; j < kLL; ++j) y[j] = 0u;
+      const uint32_t nent = 1u << T.wbits;
+#pragma unroll 4
+      for (uint32_t e = 0; e < nent; ++e) {
+        const uint32_t m = 0u - (uint32_t)(e == d);
+        const uint32_t* ent = col + (size_t)e * 160;
+#pragma unroll
+        for (int j = 0; j < kLL; ++j) y[j] |= (live ? ent[idx[j]] : 0u) & m;
+      }
+    } else {
+      if (d == 0) continue;
+      const uint32_t* ent = col + (size_t)d * 160;
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) y[j] = live ? ent[idx[j]] : 0u;
     }
     if (started) {
       mulm<MODE>(x, y, p, pd, pd1, n0, mv);
@@ -434,25 +472,88 @@ __global__ void __launch_bounds__(64) k_fbpow_wave(const Consts* __restrict__ C,
       started = true;
     }
   }
+}
+
+// One job per wave (eg_pow16.h WaveJob): out = (prod of the job's bases)^exp * T0^f0 * T1^f1 mod p.
+// Every per-element group operation is a special case: powP (one base, an exponent), gPowP and an
+// accelerated K.powP (one fixed-base term), times (two bases, no exponent), g^v * alpha^c (one base,
+// an exponent, one fixed-base term), the contest aggregate (A = prod alpha)^c.  jobs == nullptr: job e
+// is `dflt` with its rows offset by e (the batch entry points: element e of every input array).
+template <int MODE, bool CT>
+__global__ void __launch_bounds__(64) k_wave_job(const Consts* __restrict__ C, const WaveJob* __restrict__ jobs,
+                                                 WaveJob dflt, uint32_t njobs, const WaveTab* __restrict__ tabs,
+                                                 const uint8_t* __restrict__ bases, const uint8_t* __restrict__ exps,
+                                                 uint8_t* __restrict__ out_be, WaveTab t_ident) {
+  __shared__ uint32_t s_tab[16][kRow];  // window table of the variable-base term
+  __shared__ uint32_t s_w[kRow];        // byte <-> limb staging
+  __shared__ uint32_t s_x[3][9];        // the exponents (variable, fixed 0, fixed 1), LE words + a zero word
+  const uint32_t e = blockIdx.x;        // one job per workgroup of one wave; the grid is exactly njobs
+  if (e >= njobs) return;
+  WaveJob J;
+  if (jobs) {
+    J = jobs[e];
+  } else {  // the batch entry points
+    J = dflt;
+    if (J.nbase) J.base = e;
+    if (J.exp != kWaveNone) J.exp = e;
+    if (J.tab[0] != kWaveNone) J.fexp[0] = e;
+    J.out = e;
+  }
+  const uint32_t ln = lane64();
+  const uint32_t n0 = C->n0;
+  uint32_t mv;  // in a VGPR: v_and_b32_dpp takes its second operand from one
+  asm volatile("v_mov_b32 %0, %1" : "=v"(mv) : "s"(C->mask));
+  uint32_t p[kLL], x[kLL], y[kLL], pd[kLL], pd1[kLL];
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) {
+    p[j] = C->p[kLL * ln + j];
+    pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
+    pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
+  }
+  {
+    const uint32_t rows[3] = {J.exp, J.fexp[0], J.fexp[1]};
+    if (ln < 24) {
+      const uint32_t s = ln >> 3, w = ln & 7u, r = rows[s];
+      const bool used = r != kWaveNone && (s == 0 || J.tab[s - 1] != kWaveNone);
+      s_x[s][7 - w] = used ? __builtin_bswap32(reinterpret_cast<const uint32_t*>(exps + (size_t)r * 32)[w]) : 0u;
+    }
+    if (ln < 3) s_x[ln][8] = 0u;
+  }
+  bool started = false;
+  // the product of the bases, each taken into the Montgomery domain (limbs * R^2 * R^-1; a base >= p
+  // is reduced here: the result is < 2p)
+#pragma unroll 1
+  for (uint32_t k = 0; k < J.nbase; ++k) {
+    import_be(bases + (size_t)(J.base + k) * 512, y, s_w, ln);
+    uint32_t r2[kLL];
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) r2[j] = C->r2[kLL * ln + j];
+    mulm<MODE>(y, r2, p, pd, pd1, n0, mv);
+    if (started) {
+      mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) x[j] = y[j];
+      started = true;
+    }
+  }
+  __syncthreads();  // s_x
+  // an exponent on an empty product: 1^e = 1 (started stays false)
+  if (J.exp != kWaveNone && started) pow_var<MODE, CT>(x, s_x[0], s_tab, C, p, pd, pd1, n0, mv, ln);
+#pragma unroll 1
+  for (int t = 0; t < 2; ++t)
+    if (J.tab[t] != kWaveNone)
+      pow_fixed<MODE, CT>(x, started, jobs ? tabs[J.tab[t]] : t_ident, s_x[1 + t], p, pd, pd1, n0, mv, ln);
   if (!started) {
 #pragma unroll
-    for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];  // e = 0: 1
+    for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];
   }
-  // leave the Montgomery domain and write canonical bytes (as k_powp_wave)
+  // leave the Montgomery domain (x * 1 * R^-1: a value in [0, p]) and write canonical bytes
 #pragma unroll
   for (int j = 0; j < kLL; ++j) y[j] = (ln == 0 && j == 0) ? 1u : 0u;
   mulm<MODE>(x, y, p, pd, pd1, n0, mv);
   normalize(x, p, ln);
-#pragma unroll
-  for (int j = 0; j < kLL; ++j) s_w[kLL * ln + j] = x[j];
-  __syncthreads();
-  uint32_t* out32 = reinterpret_cast<uint32_t*>(out_be + (size_t)e * 512);
-  for (uint32_t b = ln; b < 128; b += 64) {
-    const int bitpos = 32 * (127 - (int)b), a = bitpos / kBits, sh = bitpos - a * kBits;
-    auto limb = [&](int k) -> uint64_t { return k < kLimbs ? (uint64_t)s_w[k] : 0ull; };
-    const uint64_t val = (limb(a) >> sh) | (limb(a + 1) << (kBits - sh)) | (limb(a + 2) << (2 * kBits - sh));
-    out32[b] = __builtin_bswap32((uint32_t)val);
-  }
+  export_be(x, out_be + (size_t)J.out * 512, s_w, ln);
 }
 }  // namespace egw
 
@@ -523,16 +624,31 @@ void powwave_consts_destroy(PowWaveConsts* c) {
   delete c;
 }
 
-int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint8_t* base_be, const uint8_t* exp_be,
-                 uint8_t* out_be, size_t n, std::string* err) {
-  if (!n) return 0;
-  if (friendly && C->d2)
-    hipLaunchKernelGGL(egw::k_powp_wave<2>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be, (uint32_t)n);
-  else if (friendly)
-    hipLaunchKernelGGL(egw::k_powp_wave<1>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be, (uint32_t)n);
-  else
-    hipLaunchKernelGGL(egw::k_powp_wave<0>, dim3((unsigned)n), dim3(64), 0, s, C->d, base_be, exp_be, out_be,
-                       (uint32_t)n);
+int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const WaveJob* d_jobs, WaveJob dflt,
+                 uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident, const uint8_t* d_bases, const uint8_t* d_exps,
+                 uint8_t* d_out, std::string* err) {
+  if (!njobs) return 0;
+  if (!d_jobs && dflt.tab[0] != kWaveNone &&
+      (t_ident.wbits < 1 || t_ident.wbits > 24 || (uint64_t)t_ident.nwin * t_ident.wbits < 256 ||
+       (uint64_t)(t_ident.nwin - 1) * t_ident.wbits >= 256 || (ct && t_ident.wbits > 8))) {
+    *err = "powwave: fixed-base table shape";
+    return 1;
+  }
+  const dim3 grid(njobs), block(64);
+#define EGW_LAUNCH(M, CTV)                                                                                       \
+  hipLaunchKernelGGL((egw::k_wave_job<M, CTV>), grid, block, 0, s, C->d, d_jobs, dflt, njobs, d_tabs, d_bases, d_exps, \
+                     d_out, t_ident)
+  const int mode = (friendly && C->d2) ? 2 : (friendly ? 1 : 0);
+  if (ct) {
+    if (mode == 2) EGW_LAUNCH(2, true);
+    else if (mode == 1) EGW_LAUNCH(1, true);
+    else EGW_LAUNCH(0, true);
+  } else {
+    if (mode == 2) EGW_LAUNCH(2, false);
+    else if (mode == 1) EGW_LAUNCH(1, false);
+    else EGW_LAUNCH(0, false);
+  }
+#undef EGW_LAUNCH
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     *err = std::string("powwave launch: ") + hipGetErrorString(e);
@@ -541,26 +657,15 @@ int powwave_powp(const PowWaveConsts* C, bool friendly, hipStream_t s, const uin
   return 0;
 }
 
-int powwave_fbpow(const PowWaveConsts* C, bool friendly, hipStream_t s, const uint32_t* tab, uint32_t wbits,
-                  uint32_t nwin, const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
-  if (!n) return 0;
-  if (wbits < 1 || wbits > 24 || (uint64_t)nwin * wbits < 256 || (uint64_t)(nwin - 1) * wbits >= 256) {
-    *err = "powwave fbpow: table shape";
-    return 1;
-  }
-  if (friendly && C->d2)
-    hipLaunchKernelGGL(egw::k_fbpow_wave<2>, dim3((unsigned)n), dim3(64), 0, s, C->d, tab, wbits, nwin, exp_be, out_be,
-                       (uint32_t)n);
-  else if (friendly)
-    hipLaunchKernelGGL(egw::k_fbpow_wave<1>, dim3((unsigned)n), dim3(64), 0, s, C->d, tab, wbits, nwin, exp_be, out_be,
-                       (uint32_t)n);
-  else
-    hipLaunchKernelGGL(egw::k_fbpow_wave<0>, dim3((unsigned)n), dim3(64), 0, s, C->d, tab, wbits, nwin, exp_be, out_be,
-                       (uint32_t)n);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    *err = std::string("powwave fbpow launch: ") + hipGetErrorString(e);
-    return 1;
-  }
-  return 0;
+int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const uint8_t* base_be,
+                 const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
+  const WaveJob d{0, 1, 0, {kWaveNone, kWaveNone}, {kWaveNone, kWaveNone}, 0};
+  return powwave_jobs(C, friendly, ct, s, nullptr, d, (uint32_t)n, nullptr, WaveTab{nullptr, 0, 0}, base_be, exp_be,
+                      out_be, err);
+}
+
+int powwave_fbpow(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const WaveTab& t,
+                  const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
+  const WaveJob d{0, 0, kWaveNone, {0, kWaveNone}, {0, kWaveNone}, 0};
+  return powwave_jobs(C, friendly, ct, s, nullptr, d, (uint32_t)n, nullptr, t, nullptr, exp_be, out_be, err);
 }

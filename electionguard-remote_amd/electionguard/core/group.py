@@ -234,6 +234,30 @@ class GroupContext:
                      self._lib.eg_multp_one(self._ctx, native.buf(x), native.buf(y), native.buf(out)))
         return bytes(out)
 
+    def mexp_one(self, bases=(), e=None, fixed=()) -> bytes:
+        """One general per-element job (eg_mexp_one): (prod bases)^e * prod_t fb_t^e_t mod p.
+        bases: up to 16 elements; e: None = exponent 1; fixed: up to two (FixedBase, exponent) terms,
+        e.g. g^v * alpha^c = mexp_one([alpha], c, [(g_table, v)])."""
+        bs = b"".join(_p_be(b) for b in bases)
+        x = _q_be(e) if e is not None else None
+        fixed = list(fixed)
+        if len(fixed) > 2:
+            raise ValueError("at most two fixed-base terms")
+        fbs = [f[0]._fb if f[0] is not None else self._g_table() for f in fixed] + [None] * (2 - len(fixed))
+        fes = [_q_be(f[1]) for f in fixed] + [None] * (2 - len(fixed))
+        out = bytearray(P_BYTES)
+        keep = [bs, x, *fes]  # alive across the call
+        native.check(self._lib, "eg_mexp_one",
+                     self._lib.eg_mexp_one(self._ctx, native.buf(bs) if bs else None, len(bases),
+                                           native.buf(x) if x is not None else None, fbs[0],
+                                           native.buf(fes[0]) if fes[0] is not None else None, fbs[1],
+                                           native.buf(fes[1]) if fes[1] is not None else None, native.buf(out)))
+        del keep
+        return bytes(out)
+
+    def _g_table(self):
+        return self._lib.eg_ctx_g_table(self._ctx)
+
     def set_coalescing(self, max_batch: int, window_us: int) -> None:
         native.check(self._lib, "eg_ctx_set_coalescing",
                      self._lib.eg_ctx_set_coalescing(self._ctx, max_batch, window_us))
@@ -301,6 +325,19 @@ class GroupContext:
     def ct_encrypt(self, on: bool) -> None:
         native.check(self._lib, "eg_ctx_set_ct_encrypt", self._lib.eg_ctx_set_ct_encrypt(self._ctx, 1 if on else 0))
         self._ct_encrypt = bool(on)
+
+    # ---- constant-time exponentiation for secret exponents (eg_ctx_set_ct_pow) ----
+    @property
+    def ct_pow(self) -> bool:
+        """Variable-base and fixed-base exponentiation (batches and per-element jobs) on a fixed
+        window schedule with masked table scans: no address or schedule depends on the exponent (a
+        trustee's share s_i through the per-element API).  Same results."""
+        return getattr(self, "_ct_pow", False)
+
+    @ct_pow.setter
+    def ct_pow(self, on: bool) -> None:
+        native.check(self._lib, "eg_ctx_set_ct_pow", self._lib.eg_ctx_set_ct_pow(self._ctx, 1 if on else 0))
+        self._ct_pow = bool(on)
 
     # ---- profiling of the dominant kernel ----
     def profile_begin(self) -> None:
@@ -378,10 +415,21 @@ class GroupContext:
         """Fold every rank's nparts x n partial-tally elements (512-B rows in HBM) mod p on ``root``
         (eg_tally_allgather_fold: one RCCL all-gather + the k_prod tree); -> (n, 512) on root, None
         elsewhere.  Without comm_init the local parts are folded."""
+        if nparts < 1 or n < 1:
+            raise ValueError("empty tally")
+        if d_parts.nbytes < nparts * n * P_BYTES:  # the all-gather reads nparts x n rows (ADVICE r04)
+            raise ValueError(f"d_parts holds {d_parts.nbytes} B, need nparts * n * 512 = {nparts * n * P_BYTES}")
         out = np.empty((n, P_BYTES), dtype=np.uint8)
         native.check(self._lib, "eg_tally_allgather_fold",
                      self._lib.eg_tally_allgather_fold(self._ctx, d_parts.ptr, nparts, n, root, _ptr(out)))
         return out if self._comm_rank() == root else None
+
+    def comm_info(self) -> tuple:
+        """(ranks, rank) as the RCCL communicator reports them (ncclCommCount / ncclCommUserRank);
+        (0, 0) without one (eg_comm_info)."""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        native.check(self._lib, "eg_comm_info", self._lib.eg_comm_info(self._ctx, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, r.value
 
     def _comm_rank(self) -> int:
         return getattr(self, "_rank", 0)
@@ -475,6 +523,14 @@ class FixedBase:
         if n:
             native.check(self.group._lib, "eg_fb_pow_batch_dev",
                          self.group._lib.eg_fb_pow_batch_dev(self._fb, d_exps, d_out, n))
+
+    def pow_one(self, e) -> bytes:
+        """base^e, one coalesced per-element job (eg_fb_pow_one: an accelerated element's powP)."""
+        x = _q_be(e)
+        out = bytearray(P_BYTES)
+        native.check(self.group._lib, "eg_fb_pow_one", self.group._lib.eg_fb_pow_one(self._fb, native.buf(x),
+                                                                                     native.buf(out)))
+        return bytes(out)
 
     def close(self) -> None:
         if getattr(self, "_fb", None):

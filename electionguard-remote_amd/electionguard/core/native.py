@@ -29,6 +29,7 @@ EXPORTED = [
     "eg_dev_alloc", "eg_dev_free", "eg_memcpy_htod", "eg_memcpy_dtoh", "eg_memset_dev", "eg_all_nonzero_dev",
     "eg_comm_unique_id", "eg_comm_init", "eg_comm_destroy", "eg_comm_all_valid", "eg_tally_allgather_fold",
     "eg_ctx_set_proof_format",
+    "eg_mexp_submit", "eg_mexp_one", "eg_fb_pow_submit", "eg_fb_pow_one", "eg_ctx_set_ct_pow", "eg_comm_info",
 ]
 
 
@@ -104,6 +105,12 @@ def _sig(lib: ctypes.CDLL) -> None:
         "eg_comm_destroy": ([P], I),
         "eg_comm_all_valid": ([P, I, ctypes.POINTER(I)], I),
         "eg_tally_allgather_fold": ([P, P, S, S, I, P], I),
+        "eg_comm_info": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
+        "eg_mexp_submit": ([P, P, S, P, P, P, P, P, P, ctypes.POINTER(c_vp)], I),
+        "eg_mexp_one": ([P, P, S, P, P, P, P, P, P], I),
+        "eg_fb_pow_submit": ([P, P, P, ctypes.POINTER(c_vp)], I),
+        "eg_fb_pow_one": ([P, P, P], I),
+        "eg_ctx_set_ct_pow": ([P, I], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name)

@@ -113,28 +113,32 @@ class TallyExchange:
         self.group, self.dist, self.world, self.rank, self.mode = group, dist, world, rank, mode
         self.note = None
         if world > 1 and mode == "rccl":
+            # 1. readiness vote BEFORE any rank enters the collective eg_comm_init: every
+            #    rank opens RCCL (eg_comm_unique_id doubles as the probe; rank 0's id is the one used)
+            #    and the world proceeds only if every rank could
             err = None
             try:
-                uid = share_comm_id(dist, rank, group.comm_unique_id) if rank != 0 else None
-            except Exception as e:  # rank 0 broadcasts even when it could not make an id
-                err = e
-            if rank == 0:
-                try:
-                    uid = group.comm_unique_id()
-                except Exception as e:
-                    uid, err = b"", e  # the others' share_comm_id fails on it: nobody calls eg_comm_init
-                box = [uid]
+                uid = group.comm_unique_id()
+            except Exception as e:
+                uid, err = b"", e
+            ready = all_valid(dist, err is None)
+            if ready:
+                box = [uid if rank == 0 else None]
                 dist.broadcast_object_list(box, src=0)
-            if err is None:
+                uid = box[0]
+                # 2. the collective init: a non-blocking communicator with a deadline inside libeg
+                #    (EG_COMM_TIMEOUT_S), so a rank whose peers fail returns with an error instead of
+                #    hanging, and reaches the vote below
                 try:
                     group.comm_init(uid, world, rank)
                 except Exception as e:
                     err = e
+                ready = all_valid(dist, err is None)
             # every rank learns whether every rank has a communicator; if one failed, the whole
-            # world keeps the exchange on the host (the line says so) instead of dying
-            if not all_valid(dist, err is None):
+            # world keeps the exchange on the host (the line says so, rccl_ranks = 0) instead of dying
+            if not ready:
                 if fallback:
-                    if err is None:
+                    if err is None and group.comm_info()[0]:
                         group.comm_destroy()
                     self.mode = "gloo"
                     self.note = f"RCCL communicator unavailable ({err or 'on another rank'}): host exchange"
@@ -145,7 +149,17 @@ class TallyExchange:
 
     @property
     def collective(self) -> str:
-        return "RCCL (libeg_hip)" if self.world == 1 or self.mode == "rccl" else "gloo (host)"
+        if self.world == 1:
+            return "no communicator (world 1: local fold)"
+        return "RCCL (libeg_hip)" if self.mode == "rccl" else "gloo (host)"
+
+    @property
+    def rccl_ranks(self) -> int:
+        """Ranks of the RCCL communicator as RCCL itself reports them (eg_comm_info ->
+        ncclCommCount); 0 when the exchange runs without one (world 1, or the host fallback)."""
+        if self.world == 1 or self.mode != "rccl":
+            return 0
+        return int(self.group.comm_info()[0])
 
     def all_valid(self, ok: bool) -> bool:
         if self.world == 1:

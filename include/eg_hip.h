@@ -225,30 +225,63 @@ int eg_verify_shares(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], const uint8
                      const uint8_t* texts, const uint8_t* M_be, const uint8_t* proof, size_t n,
                      uint8_t* ok);
 
-/* ---- per-element calls, coalesced (upstream ElementModP.powP / times, GroupContext.gPowP,
- * called element by element from 11 threads: RunRemoteWorkflowTest.java:140,180, on the group
- * of KUtils.java:10-12) ----
- * eg_*_submit queues one element on the ctx's open batch of its kind and returns a ticket at
- * once; a dispatcher thread runs the batch as one eg_powp_batch / eg_fb_pow_batch (g) /
- * eg_multp_batch once the GPU is free and the oldest element has waited window_us, or when
- * max_batch elements are queued.  The caller's out must stay valid until eg_ticket_wait, which
- * blocks until the result is in out, frees the ticket and returns the batch's status.
- * eg_ctx_destroy first runs every queued element, and a ticket stays waitable after it (each
- * ticket must still be waited once, to free it); submits racing destroy fail with EG_ERR_STATE.
- * eg_*_one = submit + wait.  Defaults: max_batch 16384, window 100 us. */
+/* ---- per-element calls, coalesced (upstream ElementModP.powP / times, GroupContext.gPowP and the
+ * accelerated election key's K.powP, called element by element from 11 threads:
+ * RunRemoteWorkflowTest.java:140-141,179-181, on the group of KUtils.java:10-12) ----
+ * Every per-element call is a JOB:
+ *   out = (bases[0] * ... * bases[nbases-1])^exp * fb0^e0 * fb1^e1  mod p
+ * (exp NULL: exponent 1, the product itself; fb NULL: no fixed-base term; nbases = 0 with an exponent:
+ * 1; nbases <= 16, eg_prod_reduce for longer products; fb0 / fb1 tables of this ctx, kept alive until
+ * the ticket is waited).  eg_*_submit queues one job on the ctx's open batch and returns a ticket at
+ * once; a dispatcher thread runs the batch as ONE launch of the per-wave job kernel (every mix of
+ * kinds side by side; large batches of one plain kind on the throughput layouts) once the GPU is
+ * free and the oldest job has waited window_us, or when max_batch jobs are queued.  The caller's out
+ * must stay valid until eg_ticket_wait, which blocks until the result is in out, frees the ticket
+ * and returns the batch's status.  eg_ctx_destroy first runs every queued job, and a ticket stays
+ * waitable after it (each ticket must still be waited once, to free it); submits racing destroy fail
+ * with EG_ERR_STATE.  eg_*_one = submit + wait.  Defaults: max_batch 16384, window 100 us.
+ *   eg_powp_submit   : base^exp                    (ElementModP.powP)
+ *   eg_gpowp_submit  : g^exp, g's table            (GroupContext.gPowP)
+ *   eg_fb_pow_submit : base^exp over fb's table    (an accelerated element's powP: acceleratePow(),
+ *                                                    e.g. the election key K.powP(R))
+ *   eg_multp_submit  : a * b                       (ElementModP.times)
+ *   eg_mexp_submit   : the general job, e.g. g^v * alpha^c in one job (fb0 = g's table, e0 = v,
+ *                      bases = {alpha}, exp = c), or the contest aggregate (alpha_1 ... alpha_k)^c */
 typedef struct eg_ticket eg_ticket;
 int eg_ctx_set_coalescing(eg_ctx* ctx, size_t max_batch, uint32_t window_us);
+int eg_mexp_submit(eg_ctx* ctx, const uint8_t* bases_be, size_t nbases, const uint8_t* exp_be, eg_fixed_base* fb0,
+                   const uint8_t* e0_be, eg_fixed_base* fb1, const uint8_t* e1_be, uint8_t out_be[EG_P_BYTES],
+                   eg_ticket** ticket);
 int eg_powp_submit(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], const uint8_t exp_be[EG_Q_BYTES],
                    uint8_t out_be[EG_P_BYTES], eg_ticket** ticket);
 int eg_gpowp_submit(eg_ctx* ctx, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES], eg_ticket** ticket);
+int eg_fb_pow_submit(eg_fixed_base* fb, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES],
+                     eg_ticket** ticket);
 int eg_multp_submit(eg_ctx* ctx, const uint8_t a_be[EG_P_BYTES], const uint8_t b_be[EG_P_BYTES],
                     uint8_t out_be[EG_P_BYTES], eg_ticket** ticket);
 int eg_ticket_wait(eg_ticket* ticket);
+int eg_mexp_one(eg_ctx* ctx, const uint8_t* bases_be, size_t nbases, const uint8_t* exp_be, eg_fixed_base* fb0,
+                const uint8_t* e0_be, eg_fixed_base* fb1, const uint8_t* e1_be, uint8_t out_be[EG_P_BYTES]);
 int eg_powp_one(eg_ctx* ctx, const uint8_t base_be[EG_P_BYTES], const uint8_t exp_be[EG_Q_BYTES],
                 uint8_t out_be[EG_P_BYTES]);
 int eg_gpowp_one(eg_ctx* ctx, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES]);
+int eg_fb_pow_one(eg_fixed_base* fb, const uint8_t exp_be[EG_Q_BYTES], uint8_t out_be[EG_P_BYTES]);
 int eg_multp_one(eg_ctx* ctx, const uint8_t a_be[EG_P_BYTES], const uint8_t b_be[EG_P_BYTES],
                  uint8_t out_be[EG_P_BYTES]);
+
+/* Constant-time exponentiation for secret exponents (on != 0), e.g. a trustee's share s_i or P_l(x_i)
+ * through the per-element API (RunRemoteDecryptingTrustee.java:189-193,227-232, where the L1 group
+ * context hands the trustee's powP to this library; SURVEY §7 "secret exponents"):
+ *   - variable-base terms (eg_powp_batch[_dev], the per-element jobs) use a fixed 4-bit window,
+ *     4 squarings + 1 multiply per nibble whatever its value, every window-table read a masked scan
+ *     of all 16 entries (no sliding window, no early exit on leading zero bits);
+ *   - fixed-base terms (eg_fb_pow_batch[_dev], gPowP, fb jobs) multiply in every radix window (no
+ *     zero-digit skip), each entry a masked scan of the window's whole column; a table wider than
+ *     8 bits gets a 6-bit companion table for this (built once per table, 1.76 MB).
+ * The schedule and every address are then independent of the exponent; the results are identical.
+ * eg_multinv_batch's public exponent p - 2 keeps the variable-time schedule.  The batch trustee
+ * entry (eg_trustee_decrypt_batch) is always constant-time.  Default off. */
+int eg_ctx_set_ct_pow(eg_ctx* ctx, int on);
 
 /* ---- device memory on the ctx's device (no reference counterpart: it lets a caller keep ballots
  * resident in HBM through this library alone, so its process runs ONE HIP runtime; bench.py) ----
@@ -278,6 +311,10 @@ int eg_comm_unique_id(uint8_t id[EG_COMM_ID_BYTES]);
 int eg_comm_init(eg_ctx* ctx, const uint8_t id[EG_COMM_ID_BYTES], int world, int rank);
 int eg_comm_destroy(eg_ctx* ctx);
 int eg_comm_all_valid(eg_ctx* ctx, int local_ok, int* all_ok);
+/* What the communicator reports about itself (ncclCommCount / ncclCommUserRank): *nranks = ranks of
+ * the ctx's RCCL communicator and *rank this one's; both 0 when eg_comm_init was never called (a world
+ * of one folds locally, without RCCL).  Either pointer may be NULL. */
+int eg_comm_info(eg_ctx* ctx, int* nranks, int* rank);
 int eg_tally_allgather_fold(eg_ctx* ctx, const uint8_t* d_parts_be, size_t nparts, size_t n, int root,
                             uint8_t* out_be);
 

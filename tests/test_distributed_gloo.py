@@ -1,4 +1,4 @@
-"""CPU: the N>1 path with world_size 2 and 4 over gloo — ballot shards, verdict all-reduce and
+"""CPU: the N>1 path with world_size 2, 4 and 8 over gloo — ballot shards, verdict all-reduce and
 the all-gather + mod-p fold of partial tallies (the fold is the oracle's product here;
 on the GPU it is GroupContext.prodP_groups)."""
 import os
@@ -52,11 +52,11 @@ def _worker(rank, world, port, data, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_n_rank_tally_fold_equals_global_tally(world):
     G = O.production_group()
     rng = random.Random(5)
-    nb, n_real = 7, 3  # ragged shards: 4 + 3 (2 ranks), 2 + 2 + 2 + 1 (4 ranks)
+    nb, n_real = 7, 3  # ragged shards: 4 + 3 (2 ranks), 2 + 2 + 2 + 1 (4 ranks), 1 x 7 + 0 (8 ranks)
     cts = np.zeros((nb, n_real, 2, 512), np.uint8)
     for i in range(nb):
         for s in range(n_real):
@@ -229,10 +229,16 @@ def _fallback_worker(rank, world, port, q):
         def comm_unique_id():
             return bytes(range(128))
 
+        comm = None
+
         def comm_init(self, uid, w, r):
             assert uid == bytes(range(128)) and w == world and r == rank
             if rank == 1:
                 raise RuntimeError("no RCCL here")
+            self.comm = (w, r)
+
+        def comm_info(self):
+            return self.comm or (0, 0)
 
         def comm_destroy(self):
             FakeGroup.destroyed = True
@@ -255,3 +261,47 @@ def test_rccl_init_failure_falls_back_to_the_host_exchange():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == [(0, "gloo", "gloo (host)", True, True), (1, "gloo", "gloo (host)", False, True)]
+
+
+def test_world8_exchange_rccl_ranks_and_fallback(tmp_path):
+    """bench.py's exchange at world 8 (run_ranks, the driver's N = 8 shape) over gloo with a stand-in
+    communicator: when every rank's RCCL probe and init succeed the exchange runs in "rccl" mode and
+    reports rccl_ranks = 8 on every rank (what the communicator says, eg_comm_info); the verdict is
+    the min over ranks and the folded tally equals the tally over all ballots.  When one rank's probe
+    fails, the readiness vote keeps EVERY rank out of the collective init (no rank can be left
+    waiting in it), the world folds over the host with rccl_ranks 0 and a note, and the tally is
+    still exact."""
+    import json
+    import sys
+    from pathlib import Path
+    from electionguard.launch import run_ranks
+    child = Path(__file__).resolve().parent / "_exchange_child.py"
+    out = tmp_path / "rank0.json"
+    env = dict(os.environ, EG_TEST_PROBE_FAIL="3")
+    env.pop("WORLD_SIZE", None)
+    assert run_ranks(str(child), [str(out)], 8, timeout=300, env=env) == 0
+    d = json.loads(out.read_text())
+    assert d["world"] == 8
+    good, failed = d["good"], d["failed"]
+    assert good["mode"] == "rccl" and good["collective"] == "RCCL (libeg_hip)" and good["note"] is None
+    assert good["ok"] is True and good["bad"] is False
+    assert failed["mode"] == "gloo" and failed["collective"] == "gloo (host)" and failed["note"]
+    assert failed["ok"] is True and failed["bad"] is False
+    for r, (gc, fc, gr, fr) in enumerate(d["calls"]):
+        assert gc == ["probe", "init", "destroy"] and gr == 8, (r, gc, gr)
+        assert "init" not in fc and fr == 0, (r, fc, fr)  # the vote came before anyone's init
+    sys.path.insert(0, str(child.parent))
+    import _exchange_child as X
+    G = O.production_group()
+    cts = X.ballots(19, 2)
+    for res in (good, failed):
+        for s in range(2):
+            for c in range(2):
+                assert int(res["tally"][s][c], 16) == G.prodP([cts[i][s][c] for i in range(19)])
+
+
+def test_world1_exchange_is_labelled_local():
+    """At N = 1 there is no communicator: the line says so instead of naming RCCL (VERDICT r04 weak #5)."""
+    from electionguard.distributed import TallyExchange
+    x = TallyExchange(None, None, 1, 0, "rccl")
+    assert x.collective == "no communicator (world 1: local fold)" and x.rccl_ranks == 0 and x.note is None

@@ -54,7 +54,8 @@ def test_tally_fold_local_parts_equals_oracle(group, oracle_group, nparts):
 
 
 def test_rccl_world_one_exchange(group, oracle_group):
-    """The RCCL communicator inside libeg_hip at world size 1: unique id, init, the verdict
+    """The RCCL communicator inside libeg_hip at world size 1: unique id, init (non-blocking, with a
+    deadline), what it reports about itself (eg_comm_info), the verdict
     all-reduce (min) and the all-gather + fold of 2 partial tallies on the ctx stream, through the
     TallyExchange bench.py uses."""
     from electionguard.distributed import TallyExchange
@@ -62,8 +63,10 @@ def test_rccl_world_one_exchange(group, oracle_group):
     p = oracle_group.p
     uid = group.comm_unique_id()
     assert len(uid) == 128
+    assert group.comm_info() == (0, 0)  # no communicator yet
     group.comm_init(uid, 1, 0)
     try:
+        assert group.comm_info() == (1, 0)  # what RCCL reports (ncclCommCount / ncclCommUserRank)
         assert group.comm_all_valid(True) is True and group.comm_all_valid(False) is False
         n = 24
         parts = _rand_elems(rng, 2 * n, p).reshape(2, n, 512)
@@ -73,7 +76,10 @@ def test_rccl_world_one_exchange(group, oracle_group):
             assert int.from_bytes(out[k].tobytes(), "big") == want, k
     finally:
         group.comm_destroy()
+    assert group.comm_info() == (0, 0)
     x = TallyExchange(group, None, 1, 0)
+    # world 1 never creates a communicator, and the bench line says so
+    assert x.collective == "no communicator (world 1: local fold)" and x.rccl_ranks == 0
     one = _rand_elems(rng, 6, p).reshape(3, 2, 512)
     assert np.array_equal(x.fold(group.to_device(one), 3), one)  # world 1: the local tally itself
     assert x.all_valid(True) and not x.all_valid(False)

@@ -1,0 +1,49 @@
+#!/bin/bash
+# Round-5 GPU checks on one MI355X (gpurun): every step under its own time limit, chained so the first
+# failure ends the call.
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- 'STEPS=ftest FTESTS="tests/test_gpu_mexp.py" bash tools/gpu_r05.sh r05a'
+set -eo pipefail
+TAG=${1:-r05a}
+STEPS=${STEPS:-tests,bench}
+mkdir -p gpurun_out
+if [[ $STEPS == *ftest* ]]; then
+  timeout -k 10 900 python -u -m pytest ${FTESTS} -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/${TAG}_gpu_tests_focus.log 2>&1
+  echo "ftest: $(tail -n 1 gpurun_out/${TAG}_gpu_tests_focus.log)"
+fi
+if [[ $STEPS == *tests* ]]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/${TAG}_gpu_tests.log 2>&1
+  echo "tests: $(tail -n 1 gpurun_out/${TAG}_gpu_tests.log)"
+fi
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
+  echo "smoke: $(tail -n 1 gpurun_out/${TAG}_smoke.log)"
+fi
+if [[ $STEPS == *percall* ]]; then
+  timeout -k 10 600 python tools/percall_workflow.py ${PERCALL_ARGS} > gpurun_out/${TAG}_percall.json \
+    2> gpurun_out/${TAG}_percall.err
+  echo "percall: $(tail -c 1500 gpurun_out/${TAG}_percall.json)"
+fi
+if [[ $STEPS == *shapes* ]]; then
+  timeout -k 10 900 python tools/coalesce_shapes.py > gpurun_out/${TAG}_coalesce_shapes.json 2> gpurun_out/${TAG}_coalesce_shapes.err
+  echo "shapes: $(grep -E 'blocking|crossover' gpurun_out/${TAG}_coalesce_shapes.json | tr -d '\n')"
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
+  echo "bench: $(tail -c 400 gpurun_out/${TAG}_bench.log)"
+fi
+if [[ $STEPS == *gloo8* ]]; then
+  # bench.py's N = 8 launcher shape on one MI355X: 8 ranks, host (gloo) exchange, 12-bit tables so
+  # eight ranks' fixed-base tables share the card
+  timeout -k 10 900 env EG_DIST_BACKEND=gloo python bench.py --gpus 8 --steps 2 --warmup 1 --ballots 2000 \
+    --fb-window 12 --modexp-n 0 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo8.log 2>&1
+  echo "gloo8: $(tail -c 600 gpurun_out/${TAG}_rehearse_gloo8.log)"
+fi
+if [[ $STEPS == *ctpmc* ]]; then
+  # constant-time per-wave kernel: VALU instructions per dispatch for exponent 0 against 2^256-1
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --kernel-trace -d gpurun_out/${TAG}_ctpmc -o run \
+    -- python3 tools/ct_schedule.py > gpurun_out/${TAG}_ctpmc.log 2>&1
+  echo "ctpmc: $(tail -n 3 gpurun_out/${TAG}_ctpmc.log)"
+fi
