@@ -20,13 +20,15 @@
 //   Verifier / batchEncryption / accumulate     <- RunRemoteWorkflowTest.java:140-141,151,179-182
 //
 // Errors: a non-zero status from the C ABI throws ArithmeticException(eg_last_error()),
-// the JNI mapping INTEGRATION.md §2 describes.  Every mod-p operation runs on the GPU;
-// 256-bit mod-q scalar arithmetic (a few operations per proof / Lagrange coefficient) is
-// host arithmetic in U256 below.
+// the JNI mapping INTEGRATION.md §2 describes.  Every mod-p operation runs on the GPU (the
+// per-element ones deferred and merged into library jobs, see Deferred); 256-bit mod-q scalar
+// arithmetic (a few operations per proof / Lagrange coefficient, and the exponent algebra of
+// deferred elements) is host arithmetic in U256 below.
 #pragma once
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -219,10 +221,85 @@ class GroupContext;
 // Mode4096_V2 = the EG 2.0 group, a named option (eg_constants.hpp).
 enum class ProductionMode { Mode4096 = 0, Mode4096_V2 = 1 };
 
-// ElementModP: 512-byte big-endian value (common.proto:6-10), unchecked on import.
-struct ElementModP {
-  std::array<uint8_t, EG_P_BYTES> be{};
+// A fixed-base radix table on the device (eg_fixed_base_create): g's (the context's) or one made by
+// GroupContext::acceleratePow for an element upstream accelerates (the election key K,
+// ElementModP.acceleratePow()).  orderQ: base^q == 1 was checked, so exponents of this base may be
+// added, multiplied and negated mod q (the deferred algebra below).
+class FixedBase {
+ public:
+  FixedBase(eg_fixed_base* fb, bool owned, bool orderQ, const uint8_t* base_be) : fb_(fb), owned_(owned), orderQ_(orderQ) {
+    std::memcpy(base_.data(), base_be, EG_P_BYTES);
+  }
+  FixedBase(const FixedBase&) = delete;
+  FixedBase& operator=(const FixedBase&) = delete;
+  ~FixedBase() {
+    if (owned_ && fb_) eg_fixed_base_destroy(fb_);
+  }
+  eg_fixed_base* handle() const { return fb_; }
+  bool orderQ() const { return orderQ_; }
+  const uint8_t* base() const { return base_.data(); }
+
+ private:
+  eg_fixed_base* fb_;
+  bool owned_, orderQ_;
+  std::array<uint8_t, EG_P_BYTES> base_{};
+};
+using FixedBasePtr = std::shared_ptr<const FixedBase>;
+
+// The deferred value of per-element operations.  Upstream calls the group one element at a time from
+// 11 threads (ElementModP.powP / times, GroupContext.gPowP, the accelerated K.powP:
+// RunRemoteWorkflowTest.java:140-141,179-181), and each call's result is usually consumed a few calls
+// later (by a product, then a hash).  So an operation does not run when it is called: it returns an
+// element holding an EXPRESSION
+//     (b_1 * ... * b_k)^e * F0^f0 * F1^f1   (b_i resolved values, F_t registered fixed bases)
+// and products / powers of expressions are combined on the host where that is exact:
+//   * x.times(y) merges the fixed-base terms (a base that appears in both adds its exponents mod q,
+//     allowed when it has order q) and the variable parts (two products without an exponent, or two
+//     with the same exponent, concatenate their bases): g^v * alpha^c is ONE job;
+//   * x.powP(e) on a pure fixed-base expression of order-q bases multiplies its exponents by e mod q:
+//     (g^R)^c = g^(R c); on a product without an exponent it sets the exponent: (prod alpha)^c;
+//   * otherwise the operand is resolved and the result starts a new expression.
+// The first time a value is needed (byteArray, ==, a hash, isValidResidue) every expression this thread
+// created and has not merged into another is submitted (eg_mexp_submit: one job each, all in the
+// library's next coalesced batch), and the thread waits for the one it needs: one GPU round trip per
+// point where upstream's code actually looks at a value, instead of one per call.  Products of more
+// than 16 values (a tally accumulator) are reduced with eg_prod_reduce when resolved; pure products
+// (no exponent, no fixed base) are not submitted by other values' flushes, so an accumulator grows
+// on the host until it is read.  Results are the same integers as eager evaluation.
+struct Deferred {
+  struct Buf {  // the bases of product expressions; appended in place while the tail is unshared
+    std::mutex mu;
+    std::vector<std::array<uint8_t, EG_P_BYTES>> v;
+  };
+  // the expression (immutable after construction)
+  std::shared_ptr<Buf> buf;
+  size_t nb = 0;  // bases buf->v[0, nb)
+  bool hasExp = false;
+  U256 exp;
+  FixedBasePtr fb[2];
+  U256 fe[2];
+  int nfb = 0;
   const GroupContext* group = nullptr;
+  // evaluation
+  std::mutex mu;
+  int state = 0;          // 0 expression, 1 submitted, 2 value in out, 3 failed (err)
+  bool consumed = false;  // merged into a newer expression: other values' flushes skip it
+  eg_ticket* ticket = nullptr;
+  std::array<uint8_t, EG_P_BYTES> out{};
+  std::string err;
+  bool pureProduct() const { return !hasExp && nfb == 0; }
+  ~Deferred() {
+    if (ticket) eg_ticket_wait(ticket);  // the library may still write `out`
+  }
+};
+
+// ElementModP: 512-byte big-endian value (common.proto:6-10), unchecked on import; or a deferred one.
+struct ElementModP {
+  mutable std::array<uint8_t, EG_P_BYTES> be{};
+  const GroupContext* group = nullptr;
+  mutable bool have = true;                // be holds the value
+  std::shared_ptr<Deferred> def;           // the expression this value came from (kept for the algebra)
+  FixedBasePtr accel;                      // a fixed-base table of this value (acceleratePow; g)
 
   ElementModP() = default;
   ElementModP(const uint8_t* b, const GroupContext* g) : group(g) { std::memcpy(be.data(), b, EG_P_BYTES); }
@@ -238,16 +315,26 @@ struct ElementModP {
     for (int i = 0; i < 8; ++i) e.be[EG_P_BYTES - 1 - i] = (uint8_t)(x >> (8 * i));
     return e;
   }
-  const uint8_t* byteArray() const { return be.data(); }
-  std::string hex() const { return be_to_hex(be.data(), EG_P_BYTES); }
-  friend bool operator==(const ElementModP& a, const ElementModP& b) { return a.be == b.be; }
+  // the value (resolving a deferred one: see Deferred)
+  const uint8_t* byteArray() const {
+    if (!have) resolve();
+    return be.data();
+  }
+  bool pending() const { return !have; }
+  std::string hex() const { return be_to_hex(byteArray(), EG_P_BYTES); }
+  friend bool operator==(const ElementModP& a, const ElementModP& b) {
+    return std::memcmp(a.byteArray(), b.byteArray(), EG_P_BYTES) == 0;
+  }
   friend bool operator!=(const ElementModP& a, const ElementModP& b) { return !(a == b); }
 
-  // upstream per-element API (batches of one on the GPU)
+  // upstream per-element API (deferred: see Deferred)
   inline ElementModP powP(const struct ElementModQ& e) const;
   inline ElementModP times(const ElementModP& o) const;
   inline ElementModP multInv() const;
   inline ElementModP div(const ElementModP& o) const;
+  inline bool isValidResidue() const;
+  inline ElementModP acceleratePow() const;
+  inline void resolve() const;
 };
 
 // ElementModQ: 256-bit scalar (common.proto:12-16).
@@ -284,6 +371,25 @@ struct CompensatedDecryptionAndProof {  // decrypting_trustee_rpc.proto:41-45
 };
 
 // ---------------------------------------------------------------- GroupContext
+namespace detail {
+// An expression as the deferred algebra manipulates it (Deferred's fields, by value).
+struct Form {
+  std::shared_ptr<Deferred::Buf> buf;
+  size_t nb = 0;
+  bool hasExp = false;
+  U256 exp;
+  FixedBasePtr fb[2];
+  U256 fe[2];
+  int nfb = 0;
+};
+// the expressions this thread created and has not submitted (Deferred)
+inline std::vector<std::weak_ptr<Deferred>>& pendingQueue() {
+  thread_local std::vector<std::weak_ptr<Deferred>> q;
+  return q;
+}
+constexpr size_t kMaxJobBases = 16;  // eg_mexp_submit's limit; longer products go through eg_prod_reduce
+}  // namespace detail
+
 class GroupContext {
  public:
   GroupContext(const ElementModP& p, const ElementModQ& q, const ElementModP& g, int device = 0)
@@ -292,8 +398,12 @@ class GroupContext {
     check(eg_ctx_create(p.byteArray(), qb.data(), g.byteArray(), device, &ctx_), "eg_ctx_create");
     p_.group = this;
     g_.group = this;
+    // g's table is the context's; g has order q (checked once here), so g-exponents combine mod q
+    gfb_ = std::make_shared<FixedBase>(eg_ctx_g_table(ctx_), false, hasOrderQ(g_), g_.be.data());
+    g_.accel = gfb_;
   }
   ~GroupContext() {
+    accel_.clear();  // the tables go before the context
     if (ctx_) eg_ctx_destroy(ctx_);
   }
   GroupContext(const GroupContext&) = delete;
@@ -378,36 +488,147 @@ class GroupContext {
   }
 
   // ---- per-element API: the upstream call pattern (one element per call, from many threads,
-  // RunRemoteWorkflowTest.java:140,180); concurrent calls are coalesced into one GPU batch by
-  // the library (eg_powp_one / eg_gpowp_one / eg_multp_one, include/eg_hip.h) ----
+  // RunRemoteWorkflowTest.java:140-141,179-181).  Deferred (see Deferred): each call returns at
+  // once; the values are computed as ONE library job each (eg_mexp_submit, coalesced with the other
+  // threads' jobs) when the thread first needs one of them ----
   ElementModP gPowP(const ElementModQ& e) const {
-    const auto eb = e.byteArray();
-    ElementModP out;
-    out.group = this;
-    check(eg_gpowp_one(ctx_, eb.data(), out.be.data()), "eg_gpowp_one");
-    return out;
+    detail::Form f;
+    f.nfb = 1;
+    f.fb[0] = gfb_;
+    f.fe[0] = e.v;
+    return make(f);
   }
+  // b^e.  An accelerated b (acceleratePow, g) runs on its fixed-base table; a pure fixed-base
+  // expression of order-q bases scales its exponents; a product without an exponent takes e.
   ElementModP powP(const ElementModP& b, const ElementModQ& e) const {
-    const auto eb = e.byteArray();
-    ElementModP out;
-    out.group = this;
-    check(eg_powp_one(ctx_, b.byteArray(), eb.data(), out.be.data()), "eg_powp_one");
-    return out;
+    bool expr = false;
+    detail::Form f = formOf(b, &expr);
+    if (f.nb == 0 && f.nfb > 0) {
+      if (f.nfb == 1 && f.fe[0] == U256::from_u64(1)) {  // F^1 -> F^e (any order)
+        f.fe[0] = e.v;
+        return consumeAndMake(b, expr, f);
+      }
+      if (allOrderQ(f)) {
+        const U256 ee = modq_.reduce_small(e.v);
+        for (int t = 0; t < f.nfb; ++t) f.fe[t] = modq_.mul(modq_.reduce_small(f.fe[t]), ee);
+        return consumeAndMake(b, expr, f);
+      }
+    } else if (f.nb > 0 && f.nfb == 0 && !f.hasExp) {
+      f.hasExp = true;
+      f.exp = e.v;
+      return consumeAndMake(b, expr, f);
+    }
+    detail::Form v = valueForm(b);
+    v.hasExp = true;
+    v.exp = e.v;
+    return make(v);
   }
+  // a * b (upstream ElementModP.times): merged into one expression where that is exact, else a
+  // product of the two values (one job when read)
   ElementModP multP(const ElementModP& a, const ElementModP& b) const {
-    ElementModP out;
-    out.group = this;
-    check(eg_multp_one(ctx_, a.byteArray(), b.byteArray(), out.be.data()), "eg_multp_one");
+    bool ea = false, eb = false;
+    const detail::Form fa = formOf(a, &ea), fb = formOf(b, &eb);
+    if (auto m = merge(fa, fb)) {
+      if (ea) consume(a);
+      if (eb) consume(b);
+      return make(*m);
+    }
+    detail::Form p = valueForm(a);
+    append(p, valueForm(b));
+    return make(p);
+  }
+  // a^-1: a pure fixed-base expression of order-q bases negates its exponents; else a^(p-2) on the
+  // value (eg_multinv_batch, blocking)
+  ElementModP multInv(const ElementModP& a) const {
+    bool expr = false;
+    detail::Form f = formOf(a, &expr);
+    if (f.nb == 0 && f.nfb > 0 && allOrderQ(f)) {
+      for (int t = 0; t < f.nfb; ++t) f.fe[t] = modq_.neg(modq_.reduce_small(f.fe[t]));
+      return consumeAndMake(a, expr, f);
+    }
+    return multInvBatch({a})[0];
+  }
+  // upstream ElementModP.isValidResidue(): 0 <= a < p and a^q == 1 (the job joins this thread's
+  // pending ones: one round trip resolves them all)
+  bool isValidResidue(const ElementModP& a) const {
+    const uint8_t* v = a.byteArray();
+    if (std::memcmp(v, p_.be.data(), EG_P_BYTES) >= 0) return false;
+    ElementModP r = powP(ElementModP(v, this), q_);
+    const uint8_t* rv = r.byteArray();
+    for (int i = 0; i < EG_P_BYTES - 1; ++i)
+      if (rv[i]) return false;
+    return rv[EG_P_BYTES - 1] == 1;
+  }
+  // upstream ElementModP.acceleratePow(): a fixed-base radix table for a's value (window_bits wide,
+  // cached by value per context), so a.powP(e) is a fixed-base job; the base's order is checked
+  // (a^q == 1) so its exponents may combine mod q
+  ElementModP acceleratePow(const ElementModP& a, int windowBits = 12) const {
+    ElementModP out(a.byteArray(), this);
+    const std::string key((const char*)out.be.data(), EG_P_BYTES);
+    std::lock_guard<std::mutex> lk(accel_mu_);
+    auto it = accel_.find(key);
+    if (it == accel_.end()) {
+      eg_fixed_base* fb = nullptr;
+      check(eg_fixed_base_create(ctx_, out.be.data(), windowBits, &fb), "eg_fixed_base_create");
+      auto t = std::make_shared<FixedBase>(fb, true, hasOrderQ(out), out.be.data());
+      if (accel_.size() >= 8) accel_.erase(accel_.begin());  // a few keys per context
+      it = accel_.emplace(key, std::move(t)).first;
+    }
+    out.accel = it->second;
     return out;
   }
+  // off: every per-element call resolves at once (one blocking GPU round trip each; for A/B runs)
+  void setDeferred(bool on) const { deferred_ = on; }
+  bool deferred() const { return deferred_; }
+  // eg_ctx_set_ct_pow: exponentiation on the constant-time schedule (a trustee's secret exponents)
+  void setConstantTime(bool on) const { check(eg_ctx_set_ct_pow(ctx_, on ? 1 : 0), "eg_ctx_set_ct_pow"); }
   // batch window of the per-element calls (eg_ctx_set_coalescing)
   void setCoalescing(size_t maxBatch, uint32_t windowUs) const {
     check(eg_ctx_set_coalescing(ctx_, maxBatch, windowUs), "eg_ctx_set_coalescing");
   }
+
+  // Submit every expression this thread created and has not merged or submitted yet (pure products
+  // excepted: accumulators stay on the host until read), then wait for x's value.
+  void resolve(const ElementModP& x) const {
+    if (x.have) return;
+    flushThread();
+    Deferred& d = *x.def;
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (d.state == 0) submit(d);
+    if (d.state == 1) {
+      const int rc = eg_ticket_wait(d.ticket);
+      d.ticket = nullptr;
+      d.state = rc ? 3 : 2;
+      if (rc) d.err = eg_last_error();
+    }
+    if (d.state == 3) throw ArithmeticException("deferred group operation: " + d.err);
+    std::memcpy(x.be.data(), d.out.data(), EG_P_BYTES);
+    x.have = true;
+  }
+  // resolve several values with one flush: every one of them (pure products too) is submitted before
+  // the first wait, so they share the library's next batch (a hash over them, a tally read out)
+  void resolveAll(const std::vector<const ElementModP*>& xs) const {
+    flushThread();
+    for (const ElementModP* x : xs) {
+      if (x->have) continue;
+      std::lock_guard<std::mutex> lk(x->def->mu);
+      if (x->def->state == 0) submit(*x->def);
+    }
+    for (const ElementModP* x : xs) resolve(*x);
+  }
+  static void flushThread() {
+    auto& q = detail::pendingQueue();
+    for (auto& w : q) {
+      auto d = w.lock();
+      if (!d) continue;
+      std::lock_guard<std::mutex> lk(d->mu);
+      if (d->state == 0 && !d->consumed && !d->pureProduct()) d->group->submit(*d);
+    }
+    q.clear();
+  }
   ElementModP multP(const std::vector<ElementModP>& xs) const {
     return xs.empty() ? one() : prodPGroups(xs, 1, xs.size())[0];
   }
-  ElementModP multInv(const ElementModP& a) const { return multInvBatch({a})[0]; }
 
   // dLogG(T, maxResult) [upstream]: t with g^t = T, 0 <= t <= maxResult, else nullopt.
   // Baby-step giant-step; every exponentiation and product on the GPU.
@@ -472,11 +693,193 @@ class GroupContext {
   }
 
  private:
+  // ---- the deferred algebra (see Deferred) ----
+  bool hasOrderQ(const ElementModP& x) const {
+    const auto r = powPBatch({x}, {q_});
+    const uint8_t* v = r[0].byteArray();
+    for (int i = 0; i < EG_P_BYTES - 1; ++i)
+      if (v[i]) return false;
+    return v[EG_P_BYTES - 1] == 1;
+  }
+  static bool allOrderQ(const detail::Form& f) {
+    for (int t = 0; t < f.nfb; ++t)
+      if (!f.fb[t]->orderQ()) return false;
+    return true;
+  }
+  detail::Form valueForm(const ElementModP& x) const {
+    detail::Form f;
+    f.buf = std::make_shared<Deferred::Buf>();
+    f.buf->v.emplace_back();
+    std::memcpy(f.buf->v[0].data(), x.byteArray(), EG_P_BYTES);
+    f.nb = 1;
+    return f;
+  }
+  // x as an expression: an accelerated value is its table to the power 1; a deferred one its
+  // expression (a resolved one with a variable part: its value, so the work is not redone)
+  detail::Form formOf(const ElementModP& x, bool* expr) const {
+    *expr = false;
+    if (x.accel) {
+      detail::Form f;
+      f.nfb = 1;
+      f.fb[0] = x.accel;
+      f.fe[0] = U256::from_u64(1);
+      return f;
+    }
+    if (x.def && (!x.have || x.def->nb == 0)) {
+      const Deferred& d = *x.def;
+      detail::Form f;
+      f.buf = d.buf;
+      f.nb = d.nb;
+      f.hasExp = d.hasExp;
+      f.exp = d.exp;
+      f.nfb = d.nfb;
+      for (int t = 0; t < d.nfb; ++t) {
+        f.fb[t] = d.fb[t];
+        f.fe[t] = d.fe[t];
+      }
+      *expr = true;
+      return f;
+    }
+    return valueForm(x);
+  }
+  static void consume(const ElementModP& x) {
+    if (!x.def) return;
+    std::lock_guard<std::mutex> lk(x.def->mu);
+    if (x.def->state == 0) x.def->consumed = true;
+  }
+  ElementModP consumeAndMake(const ElementModP& x, bool expr, const detail::Form& f) const {
+    if (expr) consume(x);
+    return make(f);
+  }
+  // y's bases after x's: in place when x's buffer has not been extended by anyone else
+  static void append(detail::Form& x, const detail::Form& y) {
+    std::vector<std::array<uint8_t, EG_P_BYTES>> ys;
+    {
+      std::lock_guard<std::mutex> lk(y.buf->mu);
+      ys.assign(y.buf->v.begin(), y.buf->v.begin() + (std::ptrdiff_t)y.nb);
+    }
+    const std::shared_ptr<Deferred::Buf> old = x.buf;  // alive while its lock is held
+    std::lock_guard<std::mutex> lk(old->mu);
+    if (old->v.size() != x.nb) {  // another expression extended this buffer already: copy the prefix
+      auto nb = std::make_shared<Deferred::Buf>();
+      nb->v.assign(old->v.begin(), old->v.begin() + (std::ptrdiff_t)x.nb);
+      nb->v.insert(nb->v.end(), ys.begin(), ys.end());
+      x.nb += ys.size();
+      x.buf = nb;
+      return;
+    }
+    old->v.insert(old->v.end(), ys.begin(), ys.end());
+    x.nb += ys.size();
+  }
+  std::optional<detail::Form> merge(const detail::Form& x, const detail::Form& y) const {
+    if (x.nb && y.nb && (x.hasExp != y.hasExp || (x.hasExp && x.exp != y.exp))) return std::nullopt;
+    detail::Form r = x;
+    for (int t = 0; t < y.nfb; ++t) {
+      int k = 0;
+      while (k < r.nfb && r.fb[k] != y.fb[t]) ++k;
+      if (k < r.nfb) {
+        if (!r.fb[k]->orderQ()) return std::nullopt;
+        r.fe[k] = modq_.add(modq_.reduce_small(r.fe[k]), modq_.reduce_small(y.fe[t]));
+      } else {
+        if (r.nfb == 2) return std::nullopt;
+        r.fb[r.nfb] = y.fb[t];
+        r.fe[r.nfb] = y.fe[t];
+        ++r.nfb;
+      }
+    }
+    if (y.nb) {
+      if (!r.nb) {
+        r.buf = y.buf;
+        r.nb = y.nb;
+        r.hasExp = y.hasExp;
+        r.exp = y.exp;
+      } else {
+        append(r, y);
+      }
+    }
+    return r;
+  }
+  // a new deferred element for f (a trivial f is a plain value)
+  ElementModP make(const detail::Form& f0) const {
+    detail::Form f = f0;
+    if (f.nb == 0) f.hasExp = false;  // 1^e = 1
+    if (f.nb == 0 && f.nfb == 0) return ElementModP::from_u64(1, this);
+    if (f.nb == 1 && !f.hasExp && f.nfb == 0) {
+      std::lock_guard<std::mutex> lk(f.buf->mu);
+      return ElementModP(f.buf->v[0].data(), this);
+    }
+    auto d = std::make_shared<Deferred>();
+    d->buf = f.buf;
+    d->nb = f.nb;
+    d->hasExp = f.hasExp;
+    d->exp = f.exp;
+    d->nfb = f.nfb;
+    for (int t = 0; t < f.nfb; ++t) {
+      d->fb[t] = f.fb[t];
+      d->fe[t] = f.fe[t];
+    }
+    d->group = this;
+    ElementModP e;
+    e.group = this;
+    e.have = false;
+    e.def = d;
+    if (!deferred_) {
+      resolve(e);
+      return e;
+    }
+    auto& q = detail::pendingQueue();
+    q.push_back(d);
+    if (q.size() >= 4096 && (q.size() & 4095) == 0)  // drop the dead and the already-submitted
+      q.erase(std::remove_if(q.begin(), q.end(),
+                             [](const std::weak_ptr<Deferred>& w) {
+                               auto p = w.lock();
+                               return !p || p->state != 0 || p->consumed;
+                             }),
+              q.end());
+    return e;
+  }
+  // d.mu held, d.state == 0: one job (eg_mexp_submit); > 16 bases are folded first (eg_prod_reduce)
+  void submit(Deferred& d) const {
+    std::vector<uint8_t> bases;
+    size_t nb = d.nb;
+    if (nb) {
+      std::lock_guard<std::mutex> lk(d.buf->mu);
+      bases.resize(nb * EG_P_BYTES);
+      for (size_t i = 0; i < nb; ++i) std::memcpy(&bases[i * EG_P_BYTES], d.buf->v[i].data(), EG_P_BYTES);
+    }
+    int rc = EG_OK;
+    if (nb > detail::kMaxJobBases) {
+      std::vector<uint8_t> one(EG_P_BYTES);
+      rc = eg_prod_reduce(ctx_, bases.data(), 1, nb, one.data());
+      bases.swap(one);
+      nb = 1;
+    }
+    if (!rc) {
+      uint8_t eb[32], f0[32], f1[32];
+      d.exp.to_be(eb);
+      d.fe[0].to_be(f0);
+      d.fe[1].to_be(f1);
+      rc = eg_mexp_submit(ctx_, nb ? bases.data() : nullptr, nb, d.hasExp ? eb : nullptr,
+                          d.nfb > 0 ? d.fb[0]->handle() : nullptr, f0, d.nfb > 1 ? d.fb[1]->handle() : nullptr, f1,
+                          d.out.data(), &d.ticket);
+    }
+    if (rc) {
+      d.state = 3;
+      d.err = eg_last_error();
+    } else {
+      d.state = 1;
+    }
+  }
+
   ElementModP p_, g_;
   ElementModQ q_;
   ModQ modq_;
   int device_;
   eg_ctx* ctx_ = nullptr;
+  FixedBasePtr gfb_;
+  mutable std::mutex accel_mu_;
+  mutable std::map<std::string, FixedBasePtr> accel_;
+  mutable std::atomic<bool> deferred_{true};
 };
 
 inline const GroupContext& group_of(const ElementModP& e) {
@@ -487,6 +890,9 @@ inline ElementModP ElementModP::powP(const ElementModQ& e) const { return group_
 inline ElementModP ElementModP::times(const ElementModP& o) const { return group_of(*this).multP(*this, o); }
 inline ElementModP ElementModP::multInv() const { return group_of(*this).multInv(*this); }
 inline ElementModP ElementModP::div(const ElementModP& o) const { return times(o.multInv()); }
+inline bool ElementModP::isValidResidue() const { return group_of(*this).isValidResidue(*this); }
+inline ElementModP ElementModP::acceleratePow() const { return group_of(*this).acceleratePow(*this); }
+inline void ElementModP::resolve() const { group_of(*this).resolve(*this); }
 
 // ---------------------------------------------------------------- key material (synthetic)
 // The reference's remote key ceremony (RunRemoteKeyCeremony.java:200-233) is out of scope;
