@@ -228,6 +228,7 @@ struct eg_ctx {
   // the coalescer runs a batch of up to wave_max jobs on the per-wave kernel (any mix of kinds);
   // larger batches of one plain kind keep the throughput layouts (EG_WAVE_MAX overrides)
   size_t wave_max = 0;
+  bool wave_split = true;  // fixed-base windows of a per-element job over 4 waves (EG_WAVE_SPLIT=0: one wave)
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
 
@@ -728,6 +729,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
         c->latw_jobs = (size_t)cus * 4;  // one element per SIMD
       c->wave_max = c->latw_jobs;
       if (const char* wm = getenv("EG_WAVE_MAX")) c->wave_max = (size_t)std::max(0L, atol(wm));
+      if (const char* ws = getenv("EG_WAVE_SPLIT")) c->wave_split = ws[0] != '0';
     }
   }
   {  // c = 2^256 - q (mod 2^256) for the residue test x^(2^256) == x^c

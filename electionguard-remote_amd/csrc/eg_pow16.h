@@ -30,7 +30,7 @@ int pow16_powp(const Pow16Consts* C, bool friendly, bool ct, hipStream_t s, cons
                const uint8_t* base_be, const uint8_t* exp_be, uint8_t* out_be, size_t n, uint32_t* elems,
                uint32_t* outs, uint32_t* scratch, std::string* err);
 
-// One job per WAVE (eg_pow16.hip, namespace egw): 48 lanes x 3 limbs of 2^29 (the same 144 limbs and
+// One job per WAVE or per workgroup of 4 waves (eg_pow16.hip, namespace egw): 48 lanes x 3 limbs of 2^29 (the same 144 limbs and
 // Montgomery radix), lanes 48-63 holding zeros, the quotient digit broadcast with v_readlane and the
 // limb shift a wave_shl:1 DPP move.  A batch of up to one job per SIMD runs every job on its own
 // SIMD: the shortest latency a blocking per-element caller can get (the coalescer's batches).
@@ -60,9 +60,10 @@ struct WaveJob {
 // input array.  ct: the constant-time instantiation (fixed 4-bit windows with masked LDS scans for the
 // variable-base term, masked scans of every window column and no zero-digit skip for fixed-base terms,
 // whose tables must then have wbits <= 8).
-int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const WaveJob* d_jobs, WaveJob dflt,
-                 uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident, const uint8_t* d_bases, const uint8_t* d_exps,
-                 uint8_t* d_out, std::string* err);
+// waves > 1: four waves per job, the fixed-base windows split over them (eg_pow16.hip k_wave_job).
+int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, hipStream_t s, const WaveJob* d_jobs,
+                 WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident, const uint8_t* d_bases,
+                 const uint8_t* d_exps, uint8_t* d_out, std::string* err);
 // out_be[i] = base_be[i]^exp_be[i] mod p (device pointers, asynchronous on s; no scratch)
 int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const uint8_t* base_be,
                  const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err);

@@ -294,12 +294,16 @@ __device__ __forceinline__ void normalize(uint32_t (&x)[kLL], const uint32_t (&p
   (void)ln;
 }
 
+// LDS staging below is one wave's (wave 0 of a job's workgroup): in-order LDS within a wave, so a
+// compiler barrier suffices between a lane's store and another lane's load
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
+
 // 512 big-endian bytes -> this lane's three limbs, staged through s_w (the whole wave takes part)
 __device__ __forceinline__ void import_be(const uint8_t* __restrict__ be, uint32_t (&x)[kLL], uint32_t* s_w, uint32_t ln) {
   const uint32_t* be32 = reinterpret_cast<const uint32_t*>(be);
-  __syncthreads();  // s_w may still be read by the previous import
+  wsync();  // s_w may still be read by the previous import
   for (uint32_t k = ln; k < 128; k += 64) s_w[127 - k] = __builtin_bswap32(be32[k]);
-  __syncthreads();
+  wsync();
 #pragma unroll
   for (int j = 0; j < kLL; ++j) {
     const int bit = kBits * (kLL * (int)ln + j), wi = bit >> 5, sh = bit & 31;
@@ -312,10 +316,10 @@ __device__ __forceinline__ void import_be(const uint8_t* __restrict__ be, uint32
 // canonical limbs (normalize) -> 512 big-endian bytes
 __device__ __forceinline__ void export_be(const uint32_t (&x)[kLL], uint8_t* __restrict__ out_be, uint32_t* s_w,
                                           uint32_t ln) {
-  __syncthreads();
+  wsync();
 #pragma unroll
   for (int j = 0; j < kLL; ++j) s_w[kLL * ln + j] = x[j];
-  __syncthreads();
+  wsync();
   uint32_t* out32 = reinterpret_cast<uint32_t*>(out_be);
   for (uint32_t b = ln; b < 128; b += 64) {  // big-endian word b = little-endian word 127 - b
     const int bitpos = 32 * (127 - (int)b), a = bitpos / kBits, sh = bitpos - a * kBits;
@@ -347,7 +351,7 @@ __device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x,
                                         uint32_t mv, uint32_t ln) {
   uint32_t y[kLL];
   if constexpr (CT) {
-    __syncthreads();  // s_tab may still be read by a previous exponentiation
+    wsync();  // s_tab may still be read by a previous exponentiation
 #pragma unroll
     for (int j = 0; j < kLL; ++j) {
       s_tab[0][kLL * ln + j] = C->one[kLL * ln + j];
@@ -360,7 +364,7 @@ __device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x,
 #pragma unroll
       for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = y[j];
     }
-    __syncthreads();
+    wsync();
     auto select = [&](uint32_t (&dst)[kLL], uint32_t d) {
 #pragma unroll
       for (int j = 0; j < kLL; ++j) dst[j] = 0u;
@@ -382,7 +386,7 @@ __device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x,
   } else {
     uint32_t x2[kLL] = {x[0], x[1], x[2]};
     mulm<MODE>(x2, x, p, pd, pd1, n0, mv);
-    __syncthreads();
+    wsync();
 #pragma unroll
     for (int j = 0; j < kLL; ++j) s_tab[0][kLL * ln + j] = x[j];
 #pragma unroll 1
@@ -391,7 +395,7 @@ __device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x,
 #pragma unroll
       for (int j = 0; j < kLL; ++j) s_tab[k][kLL * ln + j] = x[j];
     }
-    __syncthreads();
+    wsync();
     auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_x[i >> 5]) >> (i & 31)) & 1u; };
     int i = 255;
     while (i >= 0 && !bit(i)) --i;
@@ -427,12 +431,15 @@ __device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x,
   }
 }
 
-// x <- x * T^e (or x <- T^e when !started) over a fixed-base radix table (eg_fixed_base_create: entries
-// in the Montgomery domain, 8-lane element layout, limb i at word (i / 18) * 20 + i % 18 of a 160-word
-// entry): one multiply per window.  Variable time: a zero digit skips its window.  CT: every window is
-// multiplied in, its entry a masked scan of the window's whole column (tables of <= 8 bits only).
+// x <- x * prod of the job's fixed-base windows [k0, k1) (or x <- that product when !started).  The
+// windows are T0's nw0 windows then T1's, each one multiply of a radix-table entry (eg_fixed_base_create:
+// entries in the Montgomery domain, 8-lane element layout, limb i at word (i / 18) * 20 + i % 18 of a
+// 160-word entry) selected by that window's digit of the term's exponent (s_x[1 + t]).  Variable time: a
+// zero digit skips its window.  CT: every window is multiplied in, its entry a masked scan of the
+// window's whole column (tables of <= 8 bits only).
 template <int MODE, bool CT>
-__device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, const WaveTab& T, const uint32_t* s_x,
+__device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, const WaveTab& T0, const WaveTab& T1,
+                                          uint32_t nw0, uint32_t k0, uint32_t k1, const uint32_t (*s_x)[9],
                                           const uint32_t (&p)[kLL], const uint32_t (&pd)[kLL],
                                           const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv, uint32_t ln) {
   uint32_t y[kLL];
@@ -444,8 +451,11 @@ __device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, con
   }
   const bool live = ln < (uint32_t)kLanes;
 #pragma unroll 1
-  for (uint32_t k = 0; k < T.nwin; ++k) {
-    const uint32_t d = exp_digit(s_x, k * T.wbits, T.wbits);
+  for (uint32_t kk = k0; kk < k1; ++kk) {
+    const bool second = kk >= nw0;
+    const WaveTab& T = second ? T1 : T0;
+    const uint32_t k = second ? kk - nw0 : kk;
+    const uint32_t d = exp_digit(s_x[second ? 2 : 1], k * T.wbits, T.wbits);
     const uint32_t* col = T.data + ((size_t)k << T.wbits) * 160;
     if constexpr (CT) {
 #pragma unroll
@@ -474,20 +484,27 @@ __device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, con
   }
 }
 
-// One job per wave (eg_pow16.h WaveJob): out = (prod of the job's bases)^exp * T0^f0 * T1^f1 mod p.
-// Every per-element group operation is a special case: powP (one base, an exponent), gPowP and an
-// accelerated K.powP (one fixed-base term), times (two bases, no exponent), g^v * alpha^c (one base,
-// an exponent, one fixed-base term), the contest aggregate (A = prod alpha)^c.  jobs == nullptr: job e
-// is `dflt` with its rows offset by e (the batch entry points: element e of every input array).
-template <int MODE, bool CT>
-__global__ void __launch_bounds__(64) k_wave_job(const Consts* __restrict__ C, const WaveJob* __restrict__ jobs,
-                                                 WaveJob dflt, uint32_t njobs, const WaveTab* __restrict__ tabs,
-                                                 const uint8_t* __restrict__ bases, const uint8_t* __restrict__ exps,
-                                                 uint8_t* __restrict__ out_be, WaveTab t_ident) {
-  __shared__ uint32_t s_tab[16][kRow];  // window table of the variable-base term
-  __shared__ uint32_t s_w[kRow];        // byte <-> limb staging
+// One job per workgroup of W waves (eg_pow16.h WaveJob): out = (prod of the job's bases)^exp * T0^f0 *
+// T1^f1 mod p.  Every per-element group operation is a special case: powP (one base, an exponent),
+// gPowP and an accelerated K.powP (one fixed-base term), times (two bases, no exponent), g^v * alpha^c
+// (one base, an exponent, one fixed-base term), the contest aggregate (A = prod alpha)^c.
+// Wave 0 runs the variable part (the bases' product and its exponentiation: a sequential chain); the
+// fixed-base windows, each an independent factor, are split over the other waves (all W waves when the
+// job has no variable part), each multiplying its share into a partial product; the partials meet in
+// LDS and fold in a log2(W) tree: a fixed-base term of n windows costs ~n/W + log2(W) multiplies of
+// latency instead of n.  jobs == nullptr: job e is `dflt` with its rows offset by e (the batch entry
+// points: element e of every input array).
+template <int MODE, bool CT, int W>
+__global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ C, const WaveJob* __restrict__ jobs,
+                                                     WaveJob dflt, uint32_t njobs, const WaveTab* __restrict__ tabs,
+                                                     const uint8_t* __restrict__ bases, const uint8_t* __restrict__ exps,
+                                                     uint8_t* __restrict__ out_be, WaveTab t_ident) {
+  __shared__ uint32_t s_tab[16][kRow];  // window table of the variable-base term (wave 0)
+  __shared__ uint32_t s_w[kRow];        // byte <-> limb staging (wave 0)
   __shared__ uint32_t s_x[3][9];        // the exponents (variable, fixed 0, fixed 1), LE words + a zero word
-  const uint32_t e = blockIdx.x;        // one job per workgroup of one wave; the grid is exactly njobs
+  __shared__ uint32_t s_part[W][kRow];  // the waves' partial products
+  __shared__ uint32_t s_has[W];         // ... and whether each has one
+  const uint32_t e = blockIdx.x;        // one job per workgroup; the grid is exactly njobs
   if (e >= njobs) return;
   WaveJob J;
   if (jobs) {
@@ -499,6 +516,7 @@ __global__ void __launch_bounds__(64) k_wave_job(const Consts* __restrict__ C, c
     if (J.tab[0] != kWaveNone) J.fexp[0] = e;
     J.out = e;
   }
+  const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
   const uint32_t ln = lane64();
   const uint32_t n0 = C->n0;
   uint32_t mv;  // in a VGPR: v_and_b32_dpp takes its second operand from one
@@ -510,7 +528,7 @@ __global__ void __launch_bounds__(64) k_wave_job(const Consts* __restrict__ C, c
     pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
     pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
   }
-  {
+  if (wv == 0) {
     const uint32_t rows[3] = {J.exp, J.fexp[0], J.fexp[1]};
     if (ln < 24) {
       const uint32_t s = ln >> 3, w = ln & 7u, r = rows[s];
@@ -519,31 +537,69 @@ __global__ void __launch_bounds__(64) k_wave_job(const Consts* __restrict__ C, c
     }
     if (ln < 3) s_x[ln][8] = 0u;
   }
-  bool started = false;
-  // the product of the bases, each taken into the Montgomery domain (limbs * R^2 * R^-1; a base >= p
-  // is reduced here: the result is < 2p)
-#pragma unroll 1
-  for (uint32_t k = 0; k < J.nbase; ++k) {
-    import_be(bases + (size_t)(J.base + k) * 512, y, s_w, ln);
-    uint32_t r2[kLL];
-#pragma unroll
-    for (int j = 0; j < kLL; ++j) r2[j] = C->r2[kLL * ln + j];
-    mulm<MODE>(y, r2, p, pd, pd1, n0, mv);
-    if (started) {
-      mulm<MODE>(x, y, p, pd, pd1, n0, mv);
-    } else {
-#pragma unroll
-      for (int j = 0; j < kLL; ++j) x[j] = y[j];
-      started = true;
-    }
-  }
+  const WaveTab T0 = J.tab[0] != kWaveNone ? (jobs ? tabs[J.tab[0]] : t_ident) : WaveTab{nullptr, 0, 0};
+  const WaveTab T1 = J.tab[1] != kWaveNone ? tabs[J.tab[1]] : WaveTab{nullptr, 0, 0};
+  const uint32_t nw0 = J.tab[0] != kWaveNone ? T0.nwin : 0u, nw = nw0 + (J.tab[1] != kWaveNone ? T1.nwin : 0u);
+  // an exponent on an empty product: 1^e = 1 (no variable part)
+  const bool has_var = J.nbase > 0;
   __syncthreads();  // s_x
-  // an exponent on an empty product: 1^e = 1 (started stays false)
-  if (J.exp != kWaveNone && started) pow_var<MODE, CT>(x, s_x[0], s_tab, C, p, pd, pd1, n0, mv, ln);
+  bool started = false;
+  if (wv == 0 && has_var) {
+    // the product of the bases, each taken into the Montgomery domain (limbs * R^2 * R^-1; a base
+    // >= p is reduced here: the result is < 2p)
 #pragma unroll 1
-  for (int t = 0; t < 2; ++t)
-    if (J.tab[t] != kWaveNone)
-      pow_fixed<MODE, CT>(x, started, jobs ? tabs[J.tab[t]] : t_ident, s_x[1 + t], p, pd, pd1, n0, mv, ln);
+    for (uint32_t k = 0; k < J.nbase; ++k) {
+      import_be(bases + (size_t)(J.base + k) * 512, y, s_w, ln);
+      uint32_t r2[kLL];
+#pragma unroll
+      for (int j = 0; j < kLL; ++j) r2[j] = C->r2[kLL * ln + j];
+      mulm<MODE>(y, r2, p, pd, pd1, n0, mv);
+      if (started) {
+        mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kLL; ++j) x[j] = y[j];
+        started = true;
+      }
+    }
+    if (J.exp != kWaveNone) pow_var<MODE, CT>(x, s_x[0], s_tab, C, p, pd, pd1, n0, mv, ln);
+  }
+  // this wave's share of the fixed-base windows (W = 1: all of them, after the variable part)
+  {
+    const uint32_t workers = (W > 1 && has_var) ? W - 1 : W;
+    const uint32_t widx = (W > 1 && has_var) ? wv - 1 : wv;
+    if (!(W > 1 && has_var && wv == 0) && nw)
+      pow_fixed<MODE, CT>(x, started, T0, T1, nw0, widx * nw / workers, (widx + 1) * nw / workers, s_x, p, pd,
+                          pd1, n0, mv, ln);
+  }
+  if constexpr (W > 1) {
+    // fold the partials: a log2(W) tree through LDS, every wave at every barrier
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) s_part[wv][kLL * ln + j] = x[j];
+    if (ln == 0) s_has[wv] = started ? 1u : 0u;
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t stride = 1; stride < (uint32_t)W; stride *= 2) {
+      if (wv % (2 * stride) == 0 && wv + stride < (uint32_t)W) {
+        if (__builtin_amdgcn_readfirstlane(s_has[wv + stride])) {
+#pragma unroll
+          for (int j = 0; j < kLL; ++j) y[j] = s_part[wv + stride][kLL * ln + j];
+          if (started) {
+            mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+          } else {
+#pragma unroll
+            for (int j = 0; j < kLL; ++j) x[j] = y[j];
+            started = true;
+          }
+#pragma unroll
+          for (int j = 0; j < kLL; ++j) s_part[wv][kLL * ln + j] = x[j];
+          if (ln == 0) s_has[wv] = started ? 1u : 0u;
+        }
+      }
+      __syncthreads();
+    }
+    if (wv != 0) return;
+  }
   if (!started) {
 #pragma unroll
     for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];
@@ -624,9 +680,9 @@ void powwave_consts_destroy(PowWaveConsts* c) {
   delete c;
 }
 
-int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const WaveJob* d_jobs, WaveJob dflt,
-                 uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident, const uint8_t* d_bases, const uint8_t* d_exps,
-                 uint8_t* d_out, std::string* err) {
+int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, hipStream_t s, const WaveJob* d_jobs,
+                 WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident, const uint8_t* d_bases,
+                 const uint8_t* d_exps, uint8_t* d_out, std::string* err) {
   if (!njobs) return 0;
   if (!d_jobs && dflt.tab[0] != kWaveNone &&
       (t_ident.wbits < 1 || t_ident.wbits > 24 || (uint64_t)t_ident.nwin * t_ident.wbits < 256 ||
@@ -634,20 +690,30 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, 
     *err = "powwave: fixed-base table shape";
     return 1;
   }
-  const dim3 grid(njobs), block(64);
-#define EGW_LAUNCH(M, CTV)                                                                                       \
-  hipLaunchKernelGGL((egw::k_wave_job<M, CTV>), grid, block, 0, s, C->d, d_jobs, dflt, njobs, d_tabs, d_bases, d_exps, \
-                     d_out, t_ident)
+  const dim3 grid(njobs);
+  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1)
+  const int W = waves > 1 ? 4 : 1;
+#define EGW_LAUNCH(M, CTV, WV)                                                                                    \
+  hipLaunchKernelGGL((egw::k_wave_job<M, CTV, WV>), grid, dim3(64 * WV), 0, s, C->d, d_jobs, dflt, njobs, d_tabs, \
+                     d_bases, d_exps, d_out, t_ident)
+#define EGW_LAUNCH_W(M, CTV) \
+  do {                       \
+    if (W == 4)              \
+      EGW_LAUNCH(M, CTV, 4); \
+    else                     \
+      EGW_LAUNCH(M, CTV, 1); \
+  } while (0)
   const int mode = (friendly && C->d2) ? 2 : (friendly ? 1 : 0);
   if (ct) {
-    if (mode == 2) EGW_LAUNCH(2, true);
-    else if (mode == 1) EGW_LAUNCH(1, true);
-    else EGW_LAUNCH(0, true);
+    if (mode == 2) EGW_LAUNCH_W(2, true);
+    else if (mode == 1) EGW_LAUNCH_W(1, true);
+    else EGW_LAUNCH_W(0, true);
   } else {
-    if (mode == 2) EGW_LAUNCH(2, false);
-    else if (mode == 1) EGW_LAUNCH(1, false);
-    else EGW_LAUNCH(0, false);
+    if (mode == 2) EGW_LAUNCH_W(2, false);
+    else if (mode == 1) EGW_LAUNCH_W(1, false);
+    else EGW_LAUNCH_W(0, false);
   }
+#undef EGW_LAUNCH_W
 #undef EGW_LAUNCH
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -660,12 +726,12 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, 
 int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const uint8_t* base_be,
                  const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
   const WaveJob d{0, 1, 0, {kWaveNone, kWaveNone}, {kWaveNone, kWaveNone}, 0};
-  return powwave_jobs(C, friendly, ct, s, nullptr, d, (uint32_t)n, nullptr, WaveTab{nullptr, 0, 0}, base_be, exp_be,
+  return powwave_jobs(C, friendly, ct, 1, s, nullptr, d, (uint32_t)n, nullptr, WaveTab{nullptr, 0, 0}, base_be, exp_be,
                       out_be, err);
 }
 
 int powwave_fbpow(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const WaveTab& t,
                   const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
   const WaveJob d{0, 0, kWaveNone, {0, kWaveNone}, {0, kWaveNone}, 0};
-  return powwave_jobs(C, friendly, ct, s, nullptr, d, (uint32_t)n, nullptr, t, nullptr, exp_be, out_be, err);
+  return powwave_jobs(C, friendly, ct, 4, s, nullptr, d, (uint32_t)n, nullptr, t, nullptr, exp_be, out_be, err);
 }
