@@ -508,6 +508,80 @@ JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_multpSubmit(JNIEnv* env, jc
   return submit_done(env, jt, eg_multp_submit((eg_ctx*)(intptr_t)ctx, x, y, jt->out, &jt->t));
 }
 
+/* The general per-element job (eg_mexp_submit): (prod of nbases 512-byte bases)^exp * fb0^e0 * fb1^e1.
+ * exp / e0 / e1 may be null (no exponent / no term; a term needs its table handle and its exponent). */
+JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_mexpSubmit(JNIEnv* env, jclass cls, jlong ctx, jbyteArray bases,
+                                                                jint nbases, jbyteArray exp, jlong fb0, jbyteArray e0,
+                                                                jlong fb1, jbyteArray e1) {
+  if (nbases < 0 || nbases > 16) {
+    throw_named(env, "java/lang/IllegalArgumentException", "nbases in [0, 16]");
+    return 0;
+  }
+  if ((fb0 != 0) != (e0 != NULL) || (fb1 != 0) != (e1 != NULL)) {
+    throw_named(env, "java/lang/IllegalArgumentException", "a fixed-base term needs its table and its exponent");
+    return 0;
+  }
+  uint8_t b[16 * EG_P_BYTES], x[EG_Q_BYTES], f0[EG_Q_BYTES], f1[EG_Q_BYTES];
+  if (nbases && get_fixed(env, bases, (size_t)nbases * EG_P_BYTES, b, "bases: nbases x 512 bytes")) return 0;
+  if (exp && get_fixed(env, exp, EG_Q_BYTES, x, "exp: 32 bytes")) return 0;
+  if (e0 && get_fixed(env, e0, EG_Q_BYTES, f0, "e0: 32 bytes")) return 0;
+  if (e1 && get_fixed(env, e1, EG_Q_BYTES, f1, "e1: 32 bytes")) return 0;
+  jni_ticket* jt = (jni_ticket*)calloc(1, sizeof(jni_ticket));
+  if (!jt) {
+    throw_named(env, "java/lang/OutOfMemoryError", "ticket");
+    return 0;
+  }
+  return submit_done(env, jt,
+                     eg_mexp_submit((eg_ctx*)(intptr_t)ctx, nbases ? b : NULL, (size_t)nbases, exp ? x : NULL,
+                                    (eg_fixed_base*)(intptr_t)fb0, e0 ? f0 : NULL, (eg_fixed_base*)(intptr_t)fb1,
+                                    e1 ? f1 : NULL, jt->out, &jt->t));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_mexpOne(JNIEnv* env, jclass cls, jlong ctx, jbyteArray bases,
+                                                            jint nbases, jbyteArray exp, jlong fb0, jbyteArray e0,
+                                                            jlong fb1, jbyteArray e1, jbyteArray out) {
+  if (need_len(env, out, EG_P_BYTES, 0, "out: 512 bytes")) return;
+  uint8_t b[16 * EG_P_BYTES], x[EG_Q_BYTES], f0[EG_Q_BYTES], f1[EG_Q_BYTES], o[EG_P_BYTES];
+  if (nbases < 0 || nbases > 16) {
+    throw_named(env, "java/lang/IllegalArgumentException", "nbases in [0, 16]");
+    return;
+  }
+  if (nbases && get_fixed(env, bases, (size_t)nbases * EG_P_BYTES, b, "bases: nbases x 512 bytes")) return;
+  if (exp && get_fixed(env, exp, EG_Q_BYTES, x, "exp: 32 bytes")) return;
+  if (e0 && get_fixed(env, e0, EG_Q_BYTES, f0, "e0: 32 bytes")) return;
+  if (e1 && get_fixed(env, e1, EG_Q_BYTES, f1, "e1: 32 bytes")) return;
+  if (check_rc(env, eg_mexp_one((eg_ctx*)(intptr_t)ctx, nbases ? b : NULL, (size_t)nbases, exp ? x : NULL,
+                                (eg_fixed_base*)(intptr_t)fb0, e0 ? f0 : NULL, (eg_fixed_base*)(intptr_t)fb1,
+                                e1 ? f1 : NULL, o)))
+    return;
+  (*env)->SetByteArrayRegion(env, out, 0, EG_P_BYTES, (const jbyte*)o);
+}
+
+/* an accelerated element's powP over its fixed-base table (acceleratePow: eg_fb_pow_submit) */
+JNIEXPORT jlong JNICALL Java_electionguard_gpu_EgHip_fbPowSubmit(JNIEnv* env, jclass cls, jlong fb, jbyteArray exp) {
+  uint8_t e[EG_Q_BYTES];
+  if (get_fixed(env, exp, EG_Q_BYTES, e, "exp: 32 bytes")) return 0;
+  jni_ticket* jt = (jni_ticket*)calloc(1, sizeof(jni_ticket));
+  if (!jt) {
+    throw_named(env, "java/lang/OutOfMemoryError", "ticket");
+    return 0;
+  }
+  return submit_done(env, jt, eg_fb_pow_submit((eg_fixed_base*)(intptr_t)fb, e, jt->out, &jt->t));
+}
+
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_fbPowOne(JNIEnv* env, jclass cls, jlong fb, jbyteArray exp,
+                                                             jbyteArray out) {
+  uint8_t e[EG_Q_BYTES], o[EG_P_BYTES];
+  if (get_fixed(env, exp, EG_Q_BYTES, e, "exp: 32 bytes") || need_len(env, out, EG_P_BYTES, 0, "out: 512 bytes")) return;
+  if (check_rc(env, eg_fb_pow_one((eg_fixed_base*)(intptr_t)fb, e, o))) return;
+  (*env)->SetByteArrayRegion(env, out, 0, EG_P_BYTES, (const jbyte*)o);
+}
+
+/* constant-time exponentiation for secret exponents (a trustee's context) */
+JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_setCtPow(JNIEnv* env, jclass cls, jlong ctx, jboolean on) {
+  check_rc(env, eg_ctx_set_ct_pow((eg_ctx*)(intptr_t)ctx, on ? 1 : 0));
+}
+
 /* Waits for the element's batch, copies the 512-byte result into out, frees the handle (also when
  * out is too short: the ticket is consumed either way). */
 JNIEXPORT void JNICALL Java_electionguard_gpu_EgHip_ticketWait(JNIEnv* env, jclass cls, jlong ticket, jbyteArray out) {
@@ -601,6 +675,19 @@ JNIEXPORT jboolean JNICALL Java_electionguard_gpu_EgHip_commAllValid(JNIEnv* env
   int all = 0;
   if (check_rc(env, eg_comm_all_valid((eg_ctx*)(intptr_t)ctx, ok ? 1 : 0, &all))) return JNI_FALSE;
   return all ? JNI_TRUE : JNI_FALSE;
+}
+
+/* what the RCCL communicator reports (eg_comm_info): its rank count (0 without one) and this rank */
+JNIEXPORT jint JNICALL Java_electionguard_gpu_EgHip_commRanks(JNIEnv* env, jclass cls, jlong ctx) {
+  int n = 0;
+  if (check_rc(env, eg_comm_info((eg_ctx*)(intptr_t)ctx, &n, NULL))) return 0;
+  return (jint)n;
+}
+
+JNIEXPORT jint JNICALL Java_electionguard_gpu_EgHip_commRank(JNIEnv* env, jclass cls, jlong ctx) {
+  int r = 0;
+  if (check_rc(env, eg_comm_info((eg_ctx*)(intptr_t)ctx, NULL, &r))) return 0;
+  return (jint)r;
 }
 
 /* out: n x 512 bytes on the root (may be null on the other ranks) */

@@ -133,6 +133,25 @@ public final class EgHip {
 
   public static native void ticketWait(long ticket, byte[] out512);
 
+  /**
+   * The general per-element job (eg_mexp_submit): (bases[0] * ... * bases[nbases-1])^exp *
+   * fb0^e0 * fb1^e1 mod p, e.g. g^v * alpha^c in one job; exp / e0 / e1 may be null (exponent 1 /
+   * no term; fb 0 with a null exponent).  At most 16 bases.
+   */
+  public static native long mexpSubmit(long ctx, byte[] bases, int nbases, byte[] exp32, long fb0, byte[] e0,
+                                       long fb1, byte[] e1);
+
+  public static native void mexpOne(long ctx, byte[] bases, int nbases, byte[] exp32, long fb0, byte[] e0,
+                                    long fb1, byte[] e1, byte[] out512);
+
+  /** An accelerated element's powP over its table (acceleratePow, e.g. the election key K.powP(R)). */
+  public static native long fbPowSubmit(long fb, byte[] exp32);
+
+  public static native void fbPowOne(long fb, byte[] exp32, byte[] out512);
+
+  /** Constant-time exponentiation schedules for secret exponents (eg_ctx_set_ct_pow). */
+  public static native void setCtPow(long ctx, boolean on);
+
   // ---- device memory through libeg_hip's own HIP runtime (eg_dev_*): handles are HBM addresses ----
   public static native long devAlloc(long ctx, long bytes);
 
@@ -159,5 +178,10 @@ public final class EgHip {
   public static native boolean commAllValid(long ctx, boolean ok);
 
   /** Every rank's nparts x n partial-tally rows (HBM, 512 B each) folded mod p into out on root. */
+  /** Ranks of the ctx's RCCL communicator as RCCL reports them (0 without one), and this rank. */
+  public static native int commRanks(long ctx);
+
+  public static native int commRank(long ctx);
+
   public static native void tallyAllgatherFold(long ctx, long dParts, long nparts, long n, int root, byte[] out);
 }

@@ -62,6 +62,10 @@ public final class GpuGroupContext implements AutoCloseable {
 
   @Override
   public synchronized void close() {
+    if (gTable16 != null) {
+      gTable16.close();
+      gTable16 = null;
+    }
     if (ctx != 0) {
       EgHip.ctxDestroy(ctx);
       ctx = 0;
@@ -69,6 +73,13 @@ public final class GpuGroupContext implements AutoCloseable {
   }
 
   // ------------------------------------------------------------------ wire packing
+
+  /** width big-endian bytes of be (BigInteger.toByteArray() / ElementModP.byteArray() forms). */
+  public static byte[] fixed(byte[] be, int width) {
+    byte[] out = new byte[width];
+    put(out, 0, be, width);
+    return out;
+  }
 
   static byte[] hex(String h, int width) {
     byte[] out = new byte[width];
@@ -224,6 +235,77 @@ public final class GpuGroupContext implements AutoCloseable {
     th.setDaemon(true);
     return th;
   });
+
+  // ------------------------------------------------------------------ per-element jobs (deferred)
+  // The L1 adapter (GpuProductionGroupContext.kt) defers per-element calls into expressions and
+  // submits each as ONE library job when a value is first needed (eg_mexp_submit).
+
+  /** A fixed-base radix table of one base (eg_fixed_base_create); orderQ: base^q == 1 was checked. */
+  public static final class Table implements AutoCloseable {
+    private long fb;
+    public final boolean orderQ;
+    private final boolean owned;
+
+    Table(long fb, boolean orderQ, boolean owned) { this.fb = fb; this.orderQ = orderQ; this.owned = owned; }
+
+    long handle() { return fb; }
+
+    @Override
+    public synchronized void close() {
+      if (owned && fb != 0) EgHip.fixedBaseDestroy(fb);
+      fb = 0;
+    }
+  }
+
+  /** A table of base's value (window_bits wide), its order checked (acceleratePow). */
+  public Table table(ElementModP base, int windowBits) {
+    byte[] b = new byte[EgHip.P_BYTES];
+    put(b, 0, base.byteArray(), EgHip.P_BYTES);
+    final long fb = EgHip.fixedBaseCreate(ctx, b, windowBits);
+    return new Table(fb, hasOrderQ(b), true);
+  }
+
+  private Table gTable16;
+
+  /** g's table for the per-element calls: 16 bits (15 multiplies per g^e, split over 4 waves), built once. */
+  public synchronized Table gTable() {
+    if (gTable16 == null) gTable16 = table(group.getG_MOD_P(), 16);
+    return gTable16;
+  }
+
+  private boolean hasOrderQ(byte[] base512) {
+    byte[] out = new byte[EgHip.P_BYTES];
+    EgHip.powpBatch(ctx, base512, qBytes(), out, 1);
+    for (int i = 0; i < EgHip.P_BYTES - 1; i++) if (out[i] != 0) return false;
+    return out[EgHip.P_BYTES - 1] == 1;
+  }
+
+  public byte[] qBytes() {
+    return hex(mode == ProductionMode.Mode4096_V2 ? EgConstants.Q_HEX_V2 : EgConstants.Q_HEX, EgHip.Q_BYTES);
+  }
+
+  public byte[] pBytes() {
+    return hex(mode == ProductionMode.Mode4096_V2 ? EgConstants.P_HEX_V2 : EgConstants.P_HEX, EgHip.P_BYTES);
+  }
+
+  /**
+   * Queue one job: (bases[0..nbases))^exp * t0^e0 * t1^e1 mod p (eg_mexp_submit); exp / t0 / t1 may
+   * be null.  Returns the ticket for {@link #waitJob}, which must be called exactly once.
+   */
+  public long submitJob(byte[] bases, int nbases, byte[] exp32, Table t0, byte[] e0, Table t1, byte[] e1) {
+    return EgHip.mexpSubmit(ctx, bases, nbases, exp32, t0 == null ? 0 : t0.handle(), e0,
+        t1 == null ? 0 : t1.handle(), e1);
+  }
+
+  /** The 512-byte result of a submitted job (frees the ticket). */
+  public byte[] waitJob(long ticket) {
+    byte[] out = new byte[EgHip.P_BYTES];
+    EgHip.ticketWait(ticket, out);
+    return out;
+  }
+
+  /** Constant-time exponentiation for secret exponents (a trustee's context; eg_ctx_set_ct_pow). */
+  public void setConstantTime(boolean on) { EgHip.setCtPow(ctx, on); }
 
   /** Batch window of the per-element calls (defaults: 16384 elements, 100 us). */
   public void setCoalescing(long maxBatch, int windowUs) { EgHip.setCoalescing(ctx, maxBatch, windowUs); }

@@ -315,6 +315,33 @@ int main(void) {
     Java_electionguard_gpu_EgHip_ticketWait(env, C, 0, o512);
     EXPECT("ticketWait(0)", AE);
     EXPECT_MSG("null");
+    /* the general job and the accelerated-element forms */
+    Java_electionguard_gpu_EgHip_mexpSubmit(env, C, N0, p, 17, q, 0, NULL, 0, NULL);
+    EXPECT("mexpSubmit 17 bases", IAE);
+    Java_electionguard_gpu_EgHip_mexpSubmit(env, C, N0, p, 1, q, 7, NULL, 0, NULL);
+    EXPECT("mexpSubmit table without exponent", IAE);
+    Java_electionguard_gpu_EgHip_mexpSubmit(env, C, N0, sh, 1, q, 0, NULL, 0, NULL);
+    EXPECT("mexpSubmit short bases", IAE);
+    t = Java_electionguard_gpu_EgHip_mexpSubmit(env, C, N0, p, 1, q, 0, NULL, 0, NULL);
+    EXPECT("mexpSubmit(0)", AE);
+    ++g_checks;
+    if (t) { ++g_errors; fprintf(stderr, "failed mexp submit returned a ticket\n"); }
+    Java_electionguard_gpu_EgHip_mexpOne(env, C, N0, p, 1, q, 0, NULL, 0, NULL, sh);
+    EXPECT("mexpOne short out", IAE);
+    Java_electionguard_gpu_EgHip_mexpOne(env, C, N0, p, 1, q, 0, NULL, 0, NULL, o512);
+    EXPECT("mexpOne(0)", AE);
+    Java_electionguard_gpu_EgHip_fbPowSubmit(env, C, N0, sh);
+    EXPECT("fbPowSubmit short exp", IAE);
+    Java_electionguard_gpu_EgHip_fbPowSubmit(env, C, N0, q);
+    EXPECT("fbPowSubmit(0)", AE);
+    Java_electionguard_gpu_EgHip_fbPowOne(env, C, N0, q, o512);
+    EXPECT("fbPowOne(0)", AE);
+    Java_electionguard_gpu_EgHip_setCtPow(env, C, N0, 1);
+    EXPECT("setCtPow(0)", AE);
+    Java_electionguard_gpu_EgHip_commRanks(env, C, N0);
+    EXPECT("commRanks(0)", AE);
+    Java_electionguard_gpu_EgHip_commRank(env, C, N0);
+    EXPECT("commRank(0)", AE);
   }
 
   /* ---- device memory and the tally exchange ---- */

@@ -22,7 +22,7 @@ def _exports():
 def test_jni_calls_every_c_abi_export():
     called = set(re.findall(r"\b(eg_[a-z0-9_]+)\s*\(", JNI_C.read_text()))
     exports = _exports()
-    assert len(exports) == 48
+    assert len(exports) == 54
     assert exports <= called, sorted(exports - called)
 
 

@@ -5,9 +5,10 @@ The adapter implements the upstream interfaces by delegation and overrides only 
 members (plus the constructors and constants that must hand out GPU elements).  The upstream
 member list is restated in tests/golden/upstream_group_api.json (the jar is absent: UNPINNED).
 Checked here: every override names a member of that list with its parameter and return types;
-every hot-path member is overridden and reaches the GPU context; every ElementModP argument that
-goes to an upstream or GPU operation is unwrapped first (upstream's ProductionElementModP would
-reject ours); the element constructors and constants wrap.  Mutations must be caught."""
+every hot-path member is overridden and reaches the deferred algebra (host/electionguard.hpp
+Deferred, restated in Kotlin); every ElementModP argument is wrapped into a GPU element before it
+reaches the algebra (an upstream element passed in must not escape it); every ElementModP result is
+a GPU element; the element constructors and constants wrap.  Mutations must be caught."""
 import json
 import re
 from pathlib import Path
@@ -25,7 +26,8 @@ def _classes(src: str) -> dict:
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
     out = {}
-    for m in re.finditer(r"\bclass\s+(\w+)\s*\((.*?)\)\s*:\s*(\w+)\s+by\s+\w+\s*\{", src, flags=re.S):
+    for m in re.finditer(r"\bclass\s+(\w+)\s*(?:internal\s+constructor\s*)?\(((?:(?!\bclass\b).)*?)\)\s*:\s*(\w+)"
+                         r"\s+by\s+[\w.()]+\s*\{", src, flags=re.S):
         depth, i = 1, m.end()
         while depth:
             depth += {"{": 1, "}": -1}.get(src[i], 0)
@@ -35,7 +37,7 @@ def _classes(src: str) -> dict:
 
 
 def _overrides(body: str) -> dict:
-    """name -> {kind, params, returns|type, expr} of each `override val|fun` in a class body."""
+    """name -> {kind, params, names, returns|type, expr} of each `override val|fun` in a class body."""
     res = {}
     for m in re.finditer(r"override\s+((?:infix\s+|operator\s+)*)(val|fun)\s+([\w<>.]+?)\s*(\((.*?)\))?\s*:\s*"
                          r"([\w<>?]+)\s*(?:get\(\)\s*)?=\s*([^\n]+)", body):
@@ -44,7 +46,9 @@ def _overrides(body: str) -> dict:
         if kind == "val":
             ent["type"] = typ
         else:
-            ent["params"] = [p.split(":")[1].strip() for p in params.split(",") if p.strip()] if params else []
+            ps = [p for p in params.split(",") if p.strip()] if params else []
+            ent["params"] = [p.split(":")[1].strip() for p in ps]
+            ent["names"] = [p.split(":")[0].strip() for p in ps]
             ent["returns"] = typ
         res[name] = ent
     return res
@@ -78,13 +82,13 @@ def check(src: str) -> list:
                 errs.append(f"{name}: hot-path member {m} is not overridden")
             elif target + "(" not in ov[m]["expr"]:
                 errs.append(f"{name}.{m} does not reach {target}")
-            elif not ov[m]["expr"].startswith(("wrap(", "ctx.wrap(")):
+            elif members[m].get("returns") == "ElementModP" and not ov[m]["expr"].startswith(("wrap(", "ctx.wrap(")):
                 errs.append(f"{name}.{m} returns an unwrapped upstream element")
-        # every ElementModP-typed argument handed on is unwrapped
+        # every ElementModP-typed argument is wrapped into a GPU element before the algebra sees it
         for m, ent in ov.items():
-            for p in ent.get("params", []):
-                if p == "ElementModP" and m not in ("div",) and "unwrap(" not in ent["expr"]:
-                    errs.append(f"{name}.{m} passes its ElementModP argument on without unwrap")
+            for p, n in zip(ent.get("params", []), ent.get("names", [])):
+                if p == "ElementModP" and f"wrap({n})" not in ent["expr"]:
+                    errs.append(f"{name}.{m} passes its ElementModP argument {n} on without wrap")
         if iface == "GroupContext":
             for c in ("ONE_MOD_P", "G_MOD_P", "GINV_MOD_P", "G_SQUARED_MOD_P", "binaryToElementModP"):
                 if c not in ov or "wrap(" not in ov[c]["expr"]:
@@ -96,30 +100,37 @@ def test_adapter_matches_the_upstream_members():
     assert check(KT.read_text()) == []
 
 
-@pytest.mark.parametrize("mutation", ["param", "return", "unwrap", "route", "constant", "delegation", "wrapres"])
+@pytest.mark.parametrize("mutation", ["param", "return", "unwrap", "route", "constant", "delegation", "wrapres",
+                                      "accelerate"])
 def test_checker_catches_a_broken_adapter(mutation):
     src = KT.read_text()
     rep = {
         "param": ("override infix fun powP(e: ElementModQ)", "override infix fun powP(e: ElementModP)"),
         "return": ("override fun multInv(): ElementModP", "override fun multInv(): ElementModP?"),
-        "unwrap": ("ctx.gpu.multP(inner, unwrap(other))", "ctx.gpu.multP(inner, other)"),
-        "route": ("wrap(gpu.gPowP(e))", "wrap(base.gPowP(e))"),
+        "unwrap": ("ctx.times(this, ctx.wrap(other))", "ctx.times(this, other as GpuElementModP)"),
+        "route": ("wrap(defer(Form.fixed(gpu.gTable(), big(e))))", "wrap(base.gPowP(e))"),
         "constant": ("override val G_MOD_P: ElementModP get() = wrap(base.G_MOD_P)",
                      "override val G_MOD_P: ElementModP get() = base.G_MOD_P"),
-        "delegation": (": ElementModP by inner {", ": ElementModP {"),
-        "wrapres": ("= ctx.wrap(ctx.gpu.powP(inner, e))", "= ctx.gpu.powP(inner, e)"),
+        "delegation": (": ElementModP by forwarding(cell) {", ": ElementModP {"),
+        "wrapres": ("= ctx.wrap(ctx.powP(this, e))", "= ctx.powP(this, e)"),
+        "accelerate": ("= ctx.wrap(ctx.accelerate(this))", "= this"),
     }[mutation]
     assert rep[0] in src, "mutation did not apply"
     assert check(src.replace(rep[0], rep[1], 1)) != []
 
 
 def test_hot_path_natives_exist():
-    """The GPU context methods the adapter routes to are the coalesced per-element calls."""
+    """The GPU context methods the adapter's algebra submits to: the general per-element job
+    (eg_mexp_submit) and its ticket, the per-element tables (g's 16-bit one, acceleratePow's), the
+    constant-time switch of a trustee's context, and the batch product."""
     java = (KT.parent.parent.parent.parent / "java" / "electionguard" / "gpu" / "GpuGroupContext.java").read_text()
-    for sig, native in (("public ElementModP powP(ElementModP base, ElementModQ e)", "EgHip.powpOne"),
-                        ("public ElementModP gPowP(ElementModQ e)", "EgHip.gpowpOne"),
-                        ("public ElementModP multP(ElementModP a, ElementModP b)", "EgHip.multpOne"),
-                        ("public ElementModP prodP(List<ElementModP> xs)", "EgHip.prodReduce"),
-                        ("public List<ElementModP> multInv(List<ElementModP> xs)", "EgHip.multinvBatch")):
+    for sig, native in (("public long submitJob(", "EgHip.mexpSubmit"),
+                        ("public byte[] waitJob(long ticket)", "EgHip.ticketWait"),
+                        ("public Table table(ElementModP base, int windowBits)", "EgHip.fixedBaseCreate"),
+                        ("public synchronized Table gTable()", "table(group.getG_MOD_P(), 16)"),
+                        ("public void setConstantTime(boolean on)", "EgHip.setCtPow"),
+                        ("public ElementModP prodP(List<ElementModP> xs)", "EgHip.prodReduce")):
         i = java.index(sig)
         assert native in java[i:java.index("\n  }", i)], sig
+    kt = KT.read_text()
+    assert "fun trustee(" in kt and "setConstantTime(true)" in kt  # a trustee's context is constant-time
