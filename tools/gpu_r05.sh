@@ -37,13 +37,14 @@ if [[ $STEPS == *gloo8* ]]; then
   # bench.py's N = 8 launcher shape on one MI355X: 8 ranks, host (gloo) exchange, 12-bit tables so
   # eight ranks' fixed-base tables share the card
   timeout -k 10 900 env EG_DIST_BACKEND=gloo python bench.py --gpus 8 --steps 2 --warmup 1 --ballots 2000 \
-    --fb-window 12 --modexp-n 0 --cpu-seconds 4 > gpurun_out/${TAG}_rehearse_gloo8.log 2>&1
+    --fb-window 12 > gpurun_out/${TAG}_rehearse_gloo8.log 2>&1
   echo "gloo8: $(tail -c 600 gpurun_out/${TAG}_rehearse_gloo8.log)"
 fi
 if [[ $STEPS == *ctpmc* ]]; then
   # constant-time per-wave kernel: VALU instructions per dispatch for exponent 0 against 2^256-1
   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --kernel-trace -d gpurun_out/${TAG}_ctpmc -o run \
+  timeout -k 10 420 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -d gpurun_out/${TAG}_ctpmc -o run --output-format csv \
     -- python3 tools/ct_schedule.py > gpurun_out/${TAG}_ctpmc.log 2>&1
-  echo "ctpmc: $(tail -n 3 gpurun_out/${TAG}_ctpmc.log)"
+  python3 tools/ct_schedule_summary.py gpurun_out/${TAG}_ctpmc gpurun_out/${TAG}_ctpmc.log > gpurun_out/${TAG}_ct_schedule.txt
+  echo "ctpmc: $(tail -n 8 gpurun_out/${TAG}_ct_schedule.txt)"
 fi
