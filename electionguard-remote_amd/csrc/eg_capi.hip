@@ -229,6 +229,7 @@ struct eg_ctx {
   // larger batches of one plain kind keep the throughput layouts (EG_WAVE_MAX overrides)
   size_t wave_max = 0;
   bool wave_split = true;  // fixed-base windows of a per-element job over 4 waves (EG_WAVE_SPLIT=0: one wave)
+  bool fb_lds = false;     // A/B: eg_fb_pow_batch_dev over a 7-bit table on the LDS-staged k_fb_lds (EG_FB_LDS=1)
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
 
@@ -751,6 +752,7 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     c->sel_blocks = (sc[0] == '5') ? 2u : (sc[1] == '2' ? 2u : (sc[1] == '4' ? 4u : 3u));
   }
   if (const char* tf = getenv("EG_TEST_FAIL_JOBS")) c->test_fail_jobs = atoi(tf);
+  if (const char* fl = getenv("EG_FB_LDS")) c->fb_lds = fl[0] == '1';
   if (const char* cw = getenv("EG_CT_WINDOW")) c->ct_window = std::max(4, std::min((int)kCtMaxWindow, atoi(cw)));
   {
     int cus = 0, per_cu = 0;
@@ -1216,12 +1218,28 @@ extern "C" int eg_powp_batch_dev(eg_ctx* c, const uint8_t* d_base_be, const uint
   return pow_dev(c, d_base_be, d_exp_be, d_out_be, n, nullptr);
 }
 
+// A/B only (EG_FB_LDS=1, a 7-bit table, variable time): the batch-major LDS-staged kernel k_fb_lds
+static int fb_lds_dev(eg_ctx* c, const FbTab& t, const uint8_t* d_exp_be, uint8_t* d_out_be, size_t n) {
+  if (n > kMaxBatch) return fail(EG_ERR_ARG, "batch too large");
+  uint32_t* d_o = nullptr;
+  int rc;
+  if ((rc = ws_get(c, W_E1, n * kW * 4, (void**)&d_o))) return rc;
+  const dim3 grid((unsigned)((n + kLdsGroups - 1) / kLdsGroups));
+  if (c->h.friendly)
+    hipLaunchKernelGGL(k_fb_lds<true>, grid, dim3(kLdsBlock), 0, c->stream, c->d, t.data, t.nwin, d_exp_be, (uint32_t)n, d_o);
+  else
+    hipLaunchKernelGGL(k_fb_lds<false>, grid, dim3(kLdsBlock), 0, c->stream, c->d, t.data, t.nwin, d_exp_be, (uint32_t)n, d_o);
+  HIPCHK(hipGetLastError());
+  return launch_export(c, d_o, n, d_out_be);
+}
+
 extern "C" int eg_fb_pow_batch_dev(eg_fixed_base* fb, const uint8_t* d_exp_be, uint8_t* d_out_be, size_t n) {
   if (!fb || (n && (!d_exp_be || !d_out_be))) return fail(EG_ERR_ARG, "null argument");
   if (!n) return EG_OK;
   eg_ctx* c = fb->ctx;
   Locked L(c);
   FbTab t = fb->tab();
+  if (!c->ct_pow && fb->wbits == kLdsWin && c->fb_lds) return fb_lds_dev(c, t, d_exp_be, d_out_be, n);
   if (c->ct_pow) {
     const int rc = ct_table_locked(c, fb, &t);
     if (rc) return rc;

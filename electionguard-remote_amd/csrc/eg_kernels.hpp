@@ -806,6 +806,49 @@ __global__ void __launch_bounds__(kBlock) k_fb_level(const MontConsts* __restric
 }
 
 // ---------------------------------------------------------------------------------
+// LDS-staged fixed-base powP (A/B only: EG_FB_LDS=1 on eg_fb_pow_batch_dev with a 7-bit table).
+// The north_star's plan for fixed-base g / K, batch-major: a workgroup of 96 element
+// groups walks the radix windows in order; for window k the whole workgroup first copies the
+// window's table slice (2^7 entries x 640 B = 80 KiB) from HBM / L2 into LDS, then every group
+// multiplies its accumulator by the entry its digit selects, straight out of LDS (the multiplier
+// operand of mont_mul is the LDS entry: no per-multiply copy).  Every group multiplies in every
+// window (entry 0 is the Montgomery one) so the wave stays uniform.  One workgroup per CU (the
+// slice fills half the LDS and a second would not fit beside the first's modulus copy).
+// ---------------------------------------------------------------------------------
+constexpr int kLdsWin = 7;
+constexpr int kLdsBlock = 768;                  // 12 waves: 3 per SIMD at k_pow's register budget
+constexpr int kLdsGroups = kLdsBlock / kT;      // 96 elements per workgroup
+template <bool F>
+__global__ void __launch_bounds__(kLdsBlock, 1) k_fb_lds(const MontConsts* __restrict__ C,
+                                                       const uint32_t* __restrict__ tab, uint32_t nwin,
+                                                       const uint8_t* __restrict__ exps, uint32_t n,
+                                                       uint32_t* __restrict__ out) {
+  __shared__ uint4 s_slice[((size_t)1 << kLdsWin) * kW / 4];
+  Mont<F> M;
+  M.load(C);
+  const uint32_t g = blockIdx.x * kLdsGroups + threadIdx.x / kT;
+  const bool live = g < n;
+  const uint8_t* e = exps + (size_t)(live ? g : n - 1) * 32;
+  const uint32_t* slice = reinterpret_cast<const uint32_t*>(s_slice);
+  uint32_t x[kL];
+#pragma unroll 1
+  for (uint32_t k = 0; k < nwin; ++k) {
+    __syncthreads();  // every group is done with the previous slice
+    const uint4* src = reinterpret_cast<const uint4*>(tab + ((size_t)k << kLdsWin) * kW);
+#pragma unroll 4
+    for (uint32_t i = threadIdx.x; i < ((uint32_t)1 << kLdsWin) * kW / 4; i += kLdsBlock) s_slice[i] = src[i];
+    __syncthreads();
+    const uint32_t d = be_digit(e, 32, (int)(k * kLdsWin), kLdsWin);
+    if (k == 0) {
+      load_elem(x, slice + (size_t)d * kW);
+    } else {
+      M.mul(x, slice + (size_t)d * kW);
+    }
+  }
+  if (live) store_elem(out + (size_t)g * kW, x);
+}
+
+// ---------------------------------------------------------------------------------
 // 256-bit scalar helpers (one thread per scalar).  Scalars are 32-B big-endian.
 // ---------------------------------------------------------------------------------
 struct U256 {

@@ -48,3 +48,14 @@ if [[ $STEPS == *ctpmc* ]]; then
   python3 tools/ct_schedule_summary.py gpurun_out/${TAG}_ctpmc gpurun_out/${TAG}_ctpmc.log > gpurun_out/${TAG}_ct_schedule.txt
   echo "ctpmc: $(tail -n 8 gpurun_out/${TAG}_ct_schedule.txt)"
 fi
+if [[ $STEPS == *abfb* ]]; then
+  # LDS-staged fixed-base tables against the HBM radix tables
+  timeout -k 10 600 python tools/ab_fb_lds.py ${ABFB_N:-262144} ${ABFB_ROUNDS:-5} > gpurun_out/${TAG}_ab_fb_lds.json \
+    2> gpurun_out/${TAG}_ab_fb_lds.err
+  echo "abfb: $(tail -c 900 gpurun_out/${TAG}_ab_fb_lds.json)"
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  AB_ROUNDS=1 timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_abfb_pmc -o run --output-format csv \
+    -- python3 tools/ab_fb_lds.py ${ABFB_N:-262144} > gpurun_out/${TAG}_abfb_pmc.log 2>&1
+  python3 tools/ab_fb_lds_pmc.py gpurun_out/${TAG}_abfb_pmc ${ABFB_N:-262144} > gpurun_out/${TAG}_abfb_traffic.txt
+  echo "abfb pmc: $(cat gpurun_out/${TAG}_abfb_traffic.txt)"
+fi
