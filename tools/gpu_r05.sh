@@ -59,3 +59,10 @@ if [[ $STEPS == *abfb* ]]; then
   python3 tools/ab_fb_lds_pmc.py gpurun_out/${TAG}_abfb_pmc ${ABFB_N:-262144} > gpurun_out/${TAG}_abfb_traffic.txt
   echo "abfb pmc: $(cat gpurun_out/${TAG}_abfb_traffic.txt)"
 fi
+if [[ $STEPS == *abw4* ]]; then
+  # k_pow at 4 waves/SIMD (EG_MIN_WAVES=4: 128 VGPRs, spills to AGPRs / scratch) against 3, per clock,
+  # three interleaved rounds of the configs[1] verify
+  AB_MODE=verify AB_NB=10000 AB_WB=22 timeout -k 10 1200 python tools/ab_mm.py w3= w4=-DEG_MIN_WAVES=4 w3= \
+    w4=-DEG_MIN_WAVES=4 w3= w4=-DEG_MIN_WAVES=4 > gpurun_out/${TAG}_ab_w4.log 2>&1
+  echo "abw4: $(tail -c 900 gpurun_out/${TAG}_ab_w4.log)"
+fi
