@@ -297,11 +297,35 @@ struct Deferred {
 struct ElementModP {
   mutable std::array<uint8_t, EG_P_BYTES> be{};
   const GroupContext* group = nullptr;
-  mutable bool have = true;                // be holds the value
+  // be holds the value.  Written once, under the expression's lock, with release order; a thread that
+  // sees it set (acquire) sees the bytes, so one element may be read from several threads at once
+  mutable std::atomic<bool> have{true};
   std::shared_ptr<Deferred> def;           // the expression this value came from (kept for the algebra)
   FixedBasePtr accel;                      // a fixed-base table of this value (acceleratePow; g)
 
   ElementModP() = default;
+  ElementModP(const ElementModP& o) : group(o.group), def(o.def), accel(o.accel) { copyValue(o); }
+  ElementModP(ElementModP&& o) noexcept : group(o.group), def(std::move(o.def)), accel(std::move(o.accel)) {
+    copyValue(o);
+  }
+  ElementModP& operator=(const ElementModP& o) {
+    if (this != &o) {
+      group = o.group;
+      def = o.def;
+      accel = o.accel;
+      copyValue(o);
+    }
+    return *this;
+  }
+  ElementModP& operator=(ElementModP&& o) noexcept {
+    if (this != &o) {
+      group = o.group;
+      def = std::move(o.def);
+      accel = std::move(o.accel);
+      copyValue(o);
+    }
+    return *this;
+  }
   ElementModP(const uint8_t* b, const GroupContext* g) : group(g) { std::memcpy(be.data(), b, EG_P_BYTES); }
   static ElementModP from_hex(const std::string& h, const GroupContext* g = nullptr) {
     ElementModP e;
@@ -317,10 +341,10 @@ struct ElementModP {
   }
   // the value (resolving a deferred one: see Deferred)
   const uint8_t* byteArray() const {
-    if (!have) resolve();
+    if (!have.load(std::memory_order_acquire)) resolve();
     return be.data();
   }
-  bool pending() const { return !have; }
+  bool pending() const { return !have.load(std::memory_order_acquire); }
   std::string hex() const { return be_to_hex(byteArray(), EG_P_BYTES); }
   friend bool operator==(const ElementModP& a, const ElementModP& b) {
     return std::memcmp(a.byteArray(), b.byteArray(), EG_P_BYTES) == 0;
@@ -335,6 +359,13 @@ struct ElementModP {
   inline bool isValidResidue() const;
   inline ElementModP acceleratePow() const;
   inline void resolve() const;
+
+ private:
+  void copyValue(const ElementModP& o) {
+    const bool h = o.have.load(std::memory_order_acquire);
+    if (h) be = o.be;
+    have.store(h, std::memory_order_release);
+  }
 };
 
 // ElementModQ: 256-bit scalar (common.proto:12-16).
@@ -603,10 +634,11 @@ class GroupContext {
   // Submit every expression this thread created and has not merged or submitted yet (pure products
   // excepted: accumulators stay on the host until read), then wait for x's value.
   void resolve(const ElementModP& x) const {
-    if (x.have) return;
+    if (x.have.load(std::memory_order_acquire)) return;
     flushThread();
     Deferred& d = *x.def;
     std::lock_guard<std::mutex> lk(d.mu);
+    if (x.have.load(std::memory_order_acquire)) return;  // another thread resolved this element
     if (d.state == 0) submit(d);
     if (d.state == 1) {
       const int rc = eg_ticket_wait(d.ticket);
@@ -616,14 +648,14 @@ class GroupContext {
     }
     if (d.state == 3) throw ArithmeticException("deferred group operation: " + d.err);
     std::memcpy(x.be.data(), d.out.data(), EG_P_BYTES);
-    x.have = true;
+    x.have.store(true, std::memory_order_release);
   }
   // resolve several values with one flush: every one of them (pure products too) is submitted before
   // the first wait, so they share the library's next batch (a hash over them, a tally read out)
   void resolveAll(const std::vector<const ElementModP*>& xs) const {
     flushThread();
     for (const ElementModP* x : xs) {
-      if (x->have) continue;
+      if (x->have.load(std::memory_order_acquire)) continue;
       std::lock_guard<std::mutex> lk(x->def->mu);
       if (x->def->state == 0) submit(*x->def);
     }
@@ -731,7 +763,7 @@ class GroupContext {
   // expression (a resolved one with a variable part: its value, so the work is not redone)
   detail::Form formOf(const ElementModP& x, bool* expr) const {
     *expr = false;
-    const bool is_g = !x.accel && !x.def && x.have && x.be == g_.be;
+    const bool is_g = !x.accel && !x.def && x.have.load(std::memory_order_acquire) && x.be == g_.be;
     if (x.accel || is_g) {
       detail::Form f;
       f.nfb = 1;
@@ -739,7 +771,7 @@ class GroupContext {
       f.fe[0] = U256::from_u64(1);
       return f;
     }
-    if (x.def && (!x.have || x.def->nb == 0)) {
+    if (x.def && (!x.have.load(std::memory_order_acquire) || x.def->nb == 0)) {
       const Deferred& d = *x.def;
       detail::Form f;
       f.buf = d.buf;
@@ -835,7 +867,7 @@ class GroupContext {
     d->group = this;
     ElementModP e;
     e.group = this;
-    e.have = false;
+    e.have.store(false, std::memory_order_relaxed);
     e.def = d;
     if (!deferred_) {
       resolve(e);
