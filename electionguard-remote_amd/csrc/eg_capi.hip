@@ -229,6 +229,9 @@ struct eg_ctx {
   // larger batches of one plain kind keep the throughput layouts (EG_WAVE_MAX overrides)
   size_t wave_max = 0;
   bool wave_split = true;  // fixed-base windows of a per-element job over 4 waves (EG_WAVE_SPLIT=0: one wave)
+  // per-wave batches of at most r2l_max jobs (one per CU) run their variable parts right to left over
+  // 4 waves (k_wave_job r2l; EG_WAVE_R2L=n overrides, 0 keeps the one-wave sliding window)
+  size_t r2l_max = 0;
   bool fb_lds = false;     // A/B: eg_fb_pow_batch_dev over a 7-bit table on the LDS-staged k_fb_lds (EG_FB_LDS=1)
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
@@ -726,8 +729,11 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
     if (mode != "0" && mode != "16" &&
         powwave_consts_create(p.data(), r2.data(), r.data(), c->h.n0, c->h.friendly, &c->latw, &err) == 0) {
       int cus = 0;
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
         c->latw_jobs = (size_t)cus * 4;  // one element per SIMD
+        c->r2l_max = (size_t)cus;        // one 4-wave job per CU
+      }
+      if (const char* rl = getenv("EG_WAVE_R2L")) c->r2l_max = (size_t)std::max(0L, atol(rl));
       c->wave_max = c->latw_jobs;
       if (const char* wm = getenv("EG_WAVE_MAX")) c->wave_max = (size_t)std::max(0L, atol(wm));
       if (const char* ws = getenv("EG_WAVE_SPLIT")) c->wave_split = ws[0] != '0';

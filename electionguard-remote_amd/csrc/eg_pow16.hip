@@ -431,17 +431,17 @@ __device__ __forceinline__ void pow_var(uint32_t (&x)[kLL], const uint32_t* s_x,
   }
 }
 
-// x <- x * prod of the job's fixed-base windows [k0, k1) (or x <- that product when !started).  The
-// windows are T0's nw0 windows then T1's, each one multiply of a radix-table entry (eg_fixed_base_create:
-// entries in the Montgomery domain, 8-lane element layout, limb i at word (i / 18) * 20 + i % 18 of a
-// 160-word entry) selected by that window's digit of the term's exponent (s_x[1 + t]).  Variable time: a
-// zero digit skips its window.  CT: every window is multiplied in, its entry a masked scan of the
-// window's whole column (tables of <= 8 bits only).
+// x <- x * the job's fixed-base window kk (or x <- that factor when !started).  The windows are T0's
+// nw0 windows then T1's, each one multiply of a radix-table entry (eg_fixed_base_create: entries in
+// the Montgomery domain, 8-lane element layout, limb i at word (i / 18) * 20 + i % 18 of a 160-word
+// entry) selected by that window's digit of the term's exponent (s_x[1 + t]).  Variable time: a zero
+// digit skips its window.  CT: every window is multiplied in, its entry a masked scan of the window's
+// whole column (tables of <= 8 bits only).
 template <int MODE, bool CT>
-__device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, const WaveTab& T0, const WaveTab& T1,
-                                          uint32_t nw0, uint32_t k0, uint32_t k1, const uint32_t (*s_x)[9],
-                                          const uint32_t (&p)[kLL], const uint32_t (&pd)[kLL],
-                                          const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv, uint32_t ln) {
+__device__ __forceinline__ void fixed_window(uint32_t (&x)[kLL], bool& started, const WaveTab& T0, const WaveTab& T1,
+                                             uint32_t nw0, uint32_t kk, const uint32_t (*s_x)[9],
+                                             const uint32_t (&p)[kLL], const uint32_t (&pd)[kLL],
+                                             const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv, uint32_t ln) {
   uint32_t y[kLL];
   uint32_t idx[kLL];
 #pragma unroll
@@ -450,38 +450,45 @@ __device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, con
     idx[j] = (i / 18) * 20 + i % 18;
   }
   const bool live = ln < (uint32_t)kLanes;
-#pragma unroll 1
-  for (uint32_t kk = k0; kk < k1; ++kk) {
-    const bool second = kk >= nw0;
-    const WaveTab& T = second ? T1 : T0;
-    const uint32_t k = second ? kk - nw0 : kk;
-    const uint32_t d = exp_digit(s_x[second ? 2 : 1], k * T.wbits, T.wbits);
-    const uint32_t* col = T.data + ((size_t)k << T.wbits) * 160;
-    if constexpr (CT) {
+  const bool second = kk >= nw0;
+  const WaveTab& T = second ? T1 : T0;
+  const uint32_t k = second ? kk - nw0 : kk;
+  const uint32_t d = exp_digit(s_x[second ? 2 : 1], k * T.wbits, T.wbits);
+  const uint32_t* col = T.data + ((size_t)k << T.wbits) * 160;
+  if constexpr (CT) {
 #pragma unroll
-      for (int j = 0; j < kLL; ++j) y[j] = 0u;
-      const uint32_t nent = 1u << T.wbits;
+    for (int j = 0; j < kLL; ++j) y[j] = 0u;
+    const uint32_t nent = 1u << T.wbits;
 #pragma unroll 4
-      for (uint32_t e = 0; e < nent; ++e) {
-        const uint32_t m = 0u - (uint32_t)(e == d);
-        const uint32_t* ent = col + (size_t)e * 160;
+    for (uint32_t e = 0; e < nent; ++e) {
+      const uint32_t m = 0u - (uint32_t)(e == d);
+      const uint32_t* ent = col + (size_t)e * 160;
 #pragma unroll
-        for (int j = 0; j < kLL; ++j) y[j] |= (live ? ent[idx[j]] : 0u) & m;
-      }
-    } else {
-      if (d == 0) continue;
-      const uint32_t* ent = col + (size_t)d * 160;
-#pragma unroll
-      for (int j = 0; j < kLL; ++j) y[j] = live ? ent[idx[j]] : 0u;
+      for (int j = 0; j < kLL; ++j) y[j] |= (live ? ent[idx[j]] : 0u) & m;
     }
-    if (started) {
-      mulm<MODE>(x, y, p, pd, pd1, n0, mv);
-    } else {
+  } else {
+    if (d == 0) return;
+    const uint32_t* ent = col + (size_t)d * 160;
 #pragma unroll
-      for (int j = 0; j < kLL; ++j) x[j] = y[j];
-      started = true;
-    }
+    for (int j = 0; j < kLL; ++j) y[j] = live ? ent[idx[j]] : 0u;
   }
+  if (started) {
+    mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+  } else {
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) x[j] = y[j];
+    started = true;
+  }
+}
+
+// windows [k0, k1) of fixed_window
+template <int MODE, bool CT>
+__device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, const WaveTab& T0, const WaveTab& T1,
+                                          uint32_t nw0, uint32_t k0, uint32_t k1, const uint32_t (*s_x)[9],
+                                          const uint32_t (&p)[kLL], const uint32_t (&pd)[kLL],
+                                          const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv, uint32_t ln) {
+#pragma unroll 1
+  for (uint32_t kk = k0; kk < k1; ++kk) fixed_window<MODE, CT>(x, started, T0, T1, nw0, kk, s_x, p, pd, pd1, n0, mv, ln);
 }
 
 // One job per workgroup of W waves (eg_pow16.h WaveJob): out = (prod of the job's bases)^exp * T0^f0 *
@@ -494,16 +501,26 @@ __device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, con
 // LDS and fold in a log2(W) tree: a fixed-base term of n windows costs ~n/W + log2(W) multiplies of
 // latency instead of n.  jobs == nullptr: job e is `dflt` with its rows offset by e (the batch entry
 // points: element e of every input array).
+// r2l (W > 1, variable time, a job with an exponent): the variable part runs right to left instead.
+// Wave 0 only squares, x_i = x^(2^i) for i up to the exponent's top bit, W - 1 squarings per round,
+// and leaves each round's powers in a double-buffered LDS ring; in the next round wave k (1 <= k < W)
+// multiplies x_i with i = (round - 1)(W - 1) + k - 1 into its partial when bit i is set, then takes one
+// of its fixed-base windows.  A wave does at most 2 multiplies while wave 0 does W - 1 = 3 squarings,
+// so the chain never waits: the latency is the top bit + ~4 operations against ~16 (window table) +
+// the top bit + ~43 (window multiplies) for the left-to-right sliding window (one SIMD per wave: the
+// waves issue side by side).  The host enables it for batches of at most one job per CU.
 template <int MODE, bool CT, int W>
 __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ C, const WaveJob* __restrict__ jobs,
                                                      WaveJob dflt, uint32_t njobs, const WaveTab* __restrict__ tabs,
                                                      const uint8_t* __restrict__ bases, const uint8_t* __restrict__ exps,
-                                                     uint8_t* __restrict__ out_be, WaveTab t_ident) {
-  __shared__ uint32_t s_tab[16][kRow];  // window table of the variable-base term (wave 0)
-  __shared__ uint32_t s_w[kRow];        // byte <-> limb staging (wave 0)
-  __shared__ uint32_t s_x[3][9];        // the exponents (variable, fixed 0, fixed 1), LE words + a zero word
-  __shared__ uint32_t s_part[W][kRow];  // the waves' partial products
-  __shared__ uint32_t s_has[W];         // ... and whether each has one
+                                                     uint8_t* __restrict__ out_be, WaveTab t_ident, uint32_t r2l) {
+  constexpr int kRing = W > 1 ? 2 * (W - 1) : 1;
+  __shared__ uint32_t s_tab[16][kRow];     // window table of the variable-base term (wave 0)
+  __shared__ uint32_t s_w[kRow];           // byte <-> limb staging (wave 0)
+  __shared__ uint32_t s_x[3][9];           // the exponents (variable, fixed 0, fixed 1), LE words + a zero word
+  __shared__ uint32_t s_part[W][kRow];     // the waves' partial products
+  __shared__ uint32_t s_has[W];            // ... and whether each has one
+  __shared__ uint32_t s_ring[kRing][kRow];  // r2l: two rounds of the squaring chain
   const uint32_t e = blockIdx.x;        // one job per workgroup; the grid is exactly njobs
   if (e >= njobs) return;
   WaveJob J;
@@ -542,6 +559,8 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
   const uint32_t nw0 = J.tab[0] != kWaveNone ? T0.nwin : 0u, nw = nw0 + (J.tab[1] != kWaveNone ? T1.nwin : 0u);
   // an exponent on an empty product: 1^e = 1 (no variable part)
   const bool has_var = J.nbase > 0;
+  // right to left over W waves (wave-uniform: the same for every wave of the job)
+  const bool split = W > 1 && !CT && r2l && has_var && J.exp != kWaveNone;
   __syncthreads();  // s_x
   bool started = false;
   if (wv == 0 && has_var) {
@@ -562,10 +581,56 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
         started = true;
       }
     }
-    if (J.exp != kWaveNone) pow_var<MODE, CT>(x, s_x[0], s_tab, C, p, pd, pd1, n0, mv, ln);
+    if (J.exp != kWaveNone && !split) pow_var<MODE, CT>(x, s_x[0], s_tab, C, p, pd, pd1, n0, mv, ln);
+  }
+  if constexpr (W > 1 && !CT) {
+    if (split) {
+      auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_x[0][i >> 5]) >> (i & 31)) & 1u; };
+      int top = 255;
+      while (top >= 0 && !bit(top)) --top;
+      constexpr int K = W - 1;
+      const int rounds = top < 0 ? 0 : top / K + 1;
+      const uint32_t widx = wv - 1;
+      uint32_t kk = wv ? widx * nw / K : 0u;
+      const uint32_t k1 = wv ? (widx + 1) * nw / K : 0u;
+#pragma unroll 1
+      for (int r = 0; r <= rounds; ++r) {
+        if (wv == 0) {
+          // x_i for i = rK .. rK + K - 1 (x holds x_(rK - 1) squared K - 1 times ago ... x_0 = x)
+#pragma unroll 1
+          for (int k = 0; k < K; ++k) {
+            const int i = r * K + k;
+            if (r == rounds || i > top) break;
+            if (i > 0) mulm<MODE>(x, x, p, pd, pd1, n0, mv);
+#pragma unroll
+            for (int j = 0; j < kLL; ++j) s_ring[(r & 1) * K + k][kLL * ln + j] = x[j];
+          }
+        } else {
+          const int i = (r - 1) * K + (int)widx;
+          if (r > 0 && i <= top && bit(i)) {
+#pragma unroll
+            for (int j = 0; j < kLL; ++j) y[j] = s_ring[((r - 1) & 1) * K + widx][kLL * ln + j];
+            if (started) {
+              mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+            } else {
+#pragma unroll
+              for (int j = 0; j < kLL; ++j) x[j] = y[j];
+              started = true;
+            }
+          }
+          if (kk < k1) fixed_window<MODE, CT>(x, started, T0, T1, nw0, kk++, s_x, p, pd, pd1, n0, mv, ln);
+        }
+        __syncthreads();  // round r's powers are in the ring; round r - 1's slots are free again
+      }
+      if (wv) {
+        pow_fixed<MODE, CT>(x, started, T0, T1, nw0, kk, k1, s_x, p, pd, pd1, n0, mv, ln);
+      } else {
+        started = false;  // the chain itself is not a factor
+      }
+    }
   }
   // this wave's share of the fixed-base windows (W = 1: all of them, after the variable part)
-  {
+  if (!split) {
     const uint32_t workers = (W > 1 && has_var) ? W - 1 : W;
     const uint32_t widx = (W > 1 && has_var) ? wv - 1 : wv;
     if (!(W > 1 && has_var && wv == 0) && nw)
@@ -680,9 +745,9 @@ void powwave_consts_destroy(PowWaveConsts* c) {
   delete c;
 }
 
-int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, hipStream_t s, const WaveJob* d_jobs,
-                 WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident, const uint8_t* d_bases,
-                 const uint8_t* d_exps, uint8_t* d_out, std::string* err) {
+int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool r2l, hipStream_t s,
+                 const WaveJob* d_jobs, WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident,
+                 const uint8_t* d_bases, const uint8_t* d_exps, uint8_t* d_out, std::string* err) {
   if (!njobs) return 0;
   if (!d_jobs && dflt.tab[0] != kWaveNone &&
       (t_ident.wbits < 1 || t_ident.wbits > 24 || (uint64_t)t_ident.nwin * t_ident.wbits < 256 ||
@@ -691,11 +756,13 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, hipS
     return 1;
   }
   const dim3 grid(njobs);
-  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1)
+  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1); r2l (4 waves, variable
+  // time): the variable part right to left over the 4 waves
   const int W = waves > 1 ? 4 : 1;
+  const uint32_t r2l_on = (r2l && W > 1 && !ct) ? 1u : 0u;
 #define EGW_LAUNCH(M, CTV, WV)                                                                                    \
   hipLaunchKernelGGL((egw::k_wave_job<M, CTV, WV>), grid, dim3(64 * WV), 0, s, C->d, d_jobs, dflt, njobs, d_tabs, \
-                     d_bases, d_exps, d_out, t_ident)
+                     d_bases, d_exps, d_out, t_ident, r2l_on)
 #define EGW_LAUNCH_W(M, CTV) \
   do {                       \
     if (W == 4)              \
@@ -723,15 +790,16 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, hipS
   return 0;
 }
 
-int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const uint8_t* base_be,
+int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, bool r2l, hipStream_t s, const uint8_t* base_be,
                  const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
   const WaveJob d{0, 1, 0, {kWaveNone, kWaveNone}, {kWaveNone, kWaveNone}, 0};
-  return powwave_jobs(C, friendly, ct, 1, s, nullptr, d, (uint32_t)n, nullptr, WaveTab{nullptr, 0, 0}, base_be, exp_be,
-                      out_be, err);
+  const bool rl = r2l && !ct;
+  return powwave_jobs(C, friendly, ct, rl ? 4 : 1, rl, s, nullptr, d, (uint32_t)n, nullptr, WaveTab{nullptr, 0, 0},
+                      base_be, exp_be, out_be, err);
 }
 
 int powwave_fbpow(const PowWaveConsts* C, bool friendly, bool ct, hipStream_t s, const WaveTab& t,
                   const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
   const WaveJob d{0, 0, kWaveNone, {0, kWaveNone}, {0, kWaveNone}, 0};
-  return powwave_jobs(C, friendly, ct, 4, s, nullptr, d, (uint32_t)n, nullptr, t, nullptr, exp_be, out_be, err);
+  return powwave_jobs(C, friendly, ct, 4, false, s, nullptr, d, (uint32_t)n, nullptr, t, nullptr, exp_be, out_be, err);
 }

@@ -98,6 +98,28 @@ class KernelProfile:
         return (self.mont_ops - self.squarings) * MAC_PER_MUL + self.squarings * MAC_PER_SQR
 
 
+class MexpTicket:
+    """A queued per-element job (GroupContext.mexp_submit): wait() returns its 512 output bytes.  The
+    library writes `out` until the ticket is waited, so an unwaited ticket waits when collected."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self.out = bytearray(P_BYTES)
+        self.ticket = ctypes.c_void_p()
+        self._done = False
+
+    def wait(self) -> bytes:
+        if not self._done:
+            self._done = True
+            native.check(self._lib, "eg_ticket_wait", self._lib.eg_ticket_wait(self.ticket))
+        return bytes(self.out)
+
+    def __del__(self):
+        if not self._done and self.ticket:
+            self._done = True
+            self._lib.eg_ticket_wait(self.ticket)
+
+
 class GroupContext:
     """GPU-backed GroupContext (one per device; calls are thread-safe)."""
 
@@ -254,6 +276,25 @@ class GroupContext:
                                            native.buf(fes[1]) if fes[1] is not None else None, native.buf(out)))
         del keep
         return bytes(out)
+
+    def mexp_submit(self, bases=(), e=None, fixed=()) -> "MexpTicket":
+        """The job of mexp_one, queued (eg_mexp_submit: inputs are copied, the output buffer is held by the
+        ticket); jobs submitted before a wait share the coalescer's next batch.  ticket.wait() -> bytes."""
+        bs = b"".join(_p_be(b) for b in bases)
+        x = _q_be(e) if e is not None else None
+        fixed = list(fixed)
+        if len(fixed) > 2:
+            raise ValueError("at most two fixed-base terms")
+        fbs = [f[0]._fb if f[0] is not None else self._g_table() for f in fixed] + [None] * (2 - len(fixed))
+        fes = [_q_be(f[1]) for f in fixed] + [None] * (2 - len(fixed))
+        t = MexpTicket(self._lib)
+        native.check(self._lib, "eg_mexp_submit",
+                     self._lib.eg_mexp_submit(self._ctx, native.buf(bs) if bs else None, len(bases),
+                                              native.buf(x) if x is not None else None, fbs[0],
+                                              native.buf(fes[0]) if fes[0] is not None else None, fbs[1],
+                                              native.buf(fes[1]) if fes[1] is not None else None,
+                                              native.buf(t.out), ctypes.byref(t.ticket)))
+        return t
 
     def _g_table(self):
         return self._lib.eg_ctx_g_table(self._ctx)

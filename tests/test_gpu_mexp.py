@@ -147,3 +147,57 @@ def test_ct_pow_batches_bitexact(group, oracle_group, tables, n):
         assert int.from_bytes(out[i].tobytes(), "big") == pow(bases[i], exps[i], og.p), i
     for i in range(min(n, 12)):
         assert int.from_bytes(out[i].tobytes(), "big") == pow(bases[i], exps[i], og.p), i
+
+
+def _r2l_exponents(og):
+    """Top bits at every residue mod 3 (the chain's rounds take 3 powers), single bits, runs of ones,
+    and the edges."""
+    es = [0, 1, 2, 3, 4, 5, 6, 7, 8, og.q - 1, og.q, 2**256 - 1, 2**255, 2**254, 2**253]
+    es += [2**k for k in (9, 10, 11, 127, 128, 129)]
+    es += [2**k - 1 for k in (2, 3, 4, 250, 251, 252)]
+    return es
+
+
+@pytest.mark.parametrize("n", [1, 37, 256])
+def test_r2l_powp_batch_bitexact(group, oracle_group, n):
+    """Batches of at most one job per CU run the variable part right to left over four waves (wave 0
+    squares, waves 1-3 multiply in the set bits from an LDS ring): bit-exact on every top-bit position
+    class, edge exponents and edge bases."""
+    og = oracle_group
+    rng = random.Random(900 + n)
+    es = _r2l_exponents(og)
+    exps = [es[i % len(es)] if i < len(es) or rng.random() < 0.3 else rng.randrange(og.q) for i in range(n)]
+    if n == 1:
+        exps = [rng.randrange(og.q)]
+    bases = [rng.choice([0, 1, og.p - 1, og.p, og.p + 5, 2**4096 - 1]) if rng.random() < 0.15 else rng.randrange(og.p)
+             for _ in range(n)]
+    out = group.powP_batch(bases, exps)
+    bad = [i for i in range(n) if int.from_bytes(out[i].tobytes(), "big") != pow(bases[i], exps[i], og.p)]
+    assert not bad, bad[:8]
+
+
+def test_r2l_mixed_jobs_bitexact(group, oracle_group, tables):
+    """Mixed per-element jobs through the coalescer on the right-to-left shape: a variable part on the
+    chain and fixed-base windows on the multiplying waves in the same rounds (g^v * alpha^c,
+    K^v * beta^c * g^-c), products of several bases raised to edge exponents, and products without an
+    exponent in the same batch."""
+    og = oracle_group
+    rng = random.Random(4242)
+    es = _r2l_exponents(og)
+    g_t, k_t, k8 = tables["g"][0], tables["K12"][0], tables["K8"][0]
+    K, K2 = tables["K12"][1], tables["K8"][1]
+    subs = []
+    for i, e in enumerate(es):
+        al = rng.randrange(og.p)
+        v = rng.randrange(og.q)
+        bases = [al] if i % 3 else [al, rng.randrange(og.p), rng.randrange(og.p)]
+        prod = 1
+        for b in bases:
+            prod = prod * b % og.p
+        subs.append((group.mexp_submit(bases, e, [(g_t, v)]), pow(prod, e, og.p) * pow(og.g, v, og.p) % og.p))
+        subs.append((group.mexp_submit(bases, e, [(k_t, v), (k8, og.q - e % og.q)]),
+                     pow(prod, e, og.p) * pow(K, v, og.p) * pow(K2, og.q - e % og.q, og.p) % og.p))
+        subs.append((group.mexp_submit(bases, e), pow(prod, e, og.p)))
+        subs.append((group.mexp_submit(bases), prod))
+    bad = [i for i, (t, want) in enumerate(subs) if int.from_bytes(t.wait(), "big") != want]
+    assert not bad, bad[:8]
