@@ -18,6 +18,7 @@
 #include <deque>
 #include <functional>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -144,6 +145,9 @@ struct eg_fixed_base {
   // constant-time companion (eg_ctx_set_ct_pow): the same base at a window a masked scan can read
   // (kCtEncWindow bits), built on first constant-time use when wbits > kCtMaxWindow; owned
   eg_fixed_base* ct = nullptr;
+  // per-element jobs queued on this table and not yet run (eg_capi_coalesce.inc): eg_fixed_base_destroy
+  // waits for them, so a queued batch never reads a freed table
+  std::atomic<int> queued{0};
   FbTab tab() const { return FbTab{d_tab, (uint32_t)wbits, (uint32_t)nwin}; }
 };
 
@@ -796,6 +800,9 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
 
 extern "C" int eg_fixed_base_destroy(eg_fixed_base* fb) {
   if (!fb) return EG_OK;
+  // jobs still queued on this table run first (the dispatcher needs no lock the caller holds: tables
+  // the library destroys under the ctx lock are never queued while it is held)
+  while (fb->queued.load(std::memory_order_acquire) > 0) std::this_thread::sleep_for(std::chrono::microseconds(20));
   if (fb->d_tab) hipFree(fb->d_tab);
   eg_fixed_base_destroy(fb->ct);
   delete fb;

@@ -201,3 +201,21 @@ def test_r2l_mixed_jobs_bitexact(group, oracle_group, tables):
         subs.append((group.mexp_submit(bases), prod))
     bad = [i for i, (t, want) in enumerate(subs) if int.from_bytes(t.wait(), "big") != want]
     assert not bad, bad[:8]
+
+
+def test_table_destroyed_with_jobs_queued(group, oracle_group):
+    """eg_fixed_base_destroy on a table with per-element jobs still queued waits until their batch
+    has run: the jobs complete bit-exact and no batch reads a freed table."""
+    og = oracle_group
+    rng = random.Random(31)
+    K = pow(og.g, rng.randrange(og.q), og.p)
+    fb = group.fixed_base(K, 8)
+    es = [rng.randrange(og.q) for _ in range(40)]
+    group.set_coalescing(4096, 20000)  # a 20 ms window: the jobs are still queued at the close
+    try:
+        ts = [group.mexp_submit([], None, [(fb, e)]) for e in es]
+        fb.close()
+        got = [int.from_bytes(t.wait(), "big") for t in ts]
+    finally:
+        group.set_coalescing(16384, 100)  # the library default
+    assert got == [pow(K, e, og.p) for e in es]
