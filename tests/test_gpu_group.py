@@ -162,3 +162,28 @@ def test_profile_counts_and_clock(group):
     assert kp.mont_ops == n * (14 + 63 * 5) and kp.squarings == n * 63 * 4
     assert kp.ms > 0 and 1.0 <= kp.clock_ghz <= 2.6, kp
     assert kp.clock_records == (n + 31) // 32 and kp.clock_dropped == 0, kp
+
+
+@pytest.mark.parametrize("n", [1, 9, 3000])
+def test_multinv_subgroup_first(group, oracle_group, n):
+    """eg_multinv_batch tries a^(q-1) (the inverse inside the order-q subgroup: a 256-bit exponent),
+    checks r * a == 1 and sends the rest to a^(p-2): subgroup elements, elements outside it (random
+    residues, p - 1 of order 2), unreduced inputs and 0 (-> 0, a^(p-2)) all come back exact, at the
+    latency shapes (n = 1, 9) and on the 8-lane batch layout (n = 3000)."""
+    O = oracle_group
+    rng = random.Random(50 + n)
+    xs = []
+    for i in range(n):
+        k = rng.random()
+        if k < 0.5:
+            xs.append(pow(O.g, rng.randrange(O.q), O.p))
+        elif k < 0.8:
+            xs.append(rng.randrange(1, O.p))
+        else:
+            xs.append(rng.choice([1, O.p - 1, 0, O.p + 1, O.p + 2, 2**4096 - 1]))
+    if n == 1:
+        xs = [pow(O.g, rng.randrange(O.q), O.p)]
+    out = group.multInv_batch(xs)
+    for i, x in enumerate(xs):
+        want = 0 if x % O.p == 0 else O.multInv(x)
+        assert be2i(out[i]) == want, (i, x % O.p == 0)
