@@ -1006,7 +1006,7 @@ __global__ void __launch_bounds__(64 * 2 * kGW) k_coop_job(const egw::Consts* __
 struct PowWaveConsts {
   egw::Consts* d = nullptr;
   bool d2 = false;  // p = -1 mod 2^58: the delayed-quotient multiply (EG_POWWAVE_D2=0 keeps mul<true>)
-  bool cyl = true;  // ... with the carry added last (EG_POWWAVE_CYL=0: before the next column's products)
+  bool cyl = false;  // ... with the carry added last (EG_POWWAVE_CYL=1; A/B)
   bool coop = false;  // p + 1 = 0 mod 2^232: the three-wave multiply for one-job-per-CU batches (EG_COOP=1)
 };
 
@@ -1060,7 +1060,7 @@ int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t*
     const char* env = std::getenv("EG_POWWAVE_D2");
     c->d2 = p[0] == 0xFFFFFFFFu && (p[1] & 0x03FFFFFFu) == 0x03FFFFFFu && !(env && env[0] == '0');
     const char* cy = std::getenv("EG_POWWAVE_CYL");
-    c->cyl = !(cy && cy[0] == '0');
+    c->cyl = cy && cy[0] == '1';
   }
   hipError_t e = hipMalloc(&c->d, sizeof(egw::Consts));
   if (e == hipSuccess) e = hipMemcpy(c->d, &h, sizeof(egw::Consts), hipMemcpyHostToDevice);
