@@ -66,12 +66,6 @@ struct WaveJob {
 int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool r2l, hipStream_t s,
                  const WaveJob* d_jobs, WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident,
                  const uint8_t* d_bases, const uint8_t* d_exps, uint8_t* d_out, std::string* err);
-// The three-wave multiply (eg_pow16.hip egc::k_coop_job: one job per workgroup of two groups of three
-// waves, a limb per lane; variable time), for p + 1 = 0 mod 2^232 (powwave_coop) and batches of at most
-// one job per CU: the same jobs and results as powwave_jobs with d_jobs.
-bool powwave_coop(const PowWaveConsts* C);
-int powwave_coop_jobs(const PowWaveConsts* C, hipStream_t s, const WaveJob* d_jobs, uint32_t njobs, const WaveTab* d_tabs,
-                      const uint8_t* d_bases, const uint8_t* d_exps, uint8_t* d_out, std::string* err);
 // out_be[i] = base_be[i]^exp_be[i] mod p (device pointers, asynchronous on s; no scratch); r2l: four
 // waves per element, right to left (ignored with ct)
 int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, bool r2l, hipStream_t s, const uint8_t* base_be,

@@ -145,9 +145,6 @@ struct Consts {
   uint32_t p[kRow], r2[kRow], one[kRow];  // limb i at [i], zeros from 144 on
   // p + 1 with its limbs shifted down by 2 (pd) and by 1 (pd1): the delayed-quotient multiply
   uint32_t pd[kRow], pd1[kRow];
-  // p + 1 shifted down by k + 1 limbs, k = 0..7 (pk[k][L] = limb L + k + 1 of p + 1): the three-wave
-  // multiply's quotient digits applied eight steps late (egc)
-  uint32_t pk[8][kRow];
   uint32_t n0;
   uint32_t mask;  // 2^29 - 1, read at run time so the AND folds into the DPP limb shift (v_and_b32_dpp)
 };
@@ -205,15 +202,9 @@ __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL]
 // MAC -> carry shift -> add, the readlane of the quotient runs beside it.  The quotient digits are the
 // standard CIOS ones (the m-terms of columns < i + 8 telescope to multiples of 2^29 for this p), so
 // the result is the same integer as mul<true>.  The last two digits are applied after the loop.
-// CYL (carry last): the retiring column's carry is kept in a register and added to the next
-// retiring column after that column's products, not before them, so a step's dependency chain is
-// the 64-bit add and the shift of the carry alone (the products run beside it); the same integer
-// sums in the same columns.  One wave per SIMD (the per-element latency shape) waits on that chain.
-template <bool CYL>
 __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&pd)[kLL],
                                        const uint32_t (&pd1)[kLL], uint32_t mv) {
   uint64_t acc[kLL] = {0, 0, 0};
-  uint64_t cy = 0;          // CYL: the carry into the next retiring column
   uint32_t m1 = 0, m2 = 0;  // quotient digits of the previous two steps
 #pragma unroll 1
   for (int q = 0; q < kLanes; ++q) {
@@ -236,23 +227,13 @@ __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[k
         A = (uint64_t)pd[j] * m2 + A;
       }
       uint64_t& A0 = acc[r];
-      if constexpr (CYL) {
-        const uint64_t t = A0 + cy;  // the retiring column, complete
-        const uint32_t m = __builtin_amdgcn_readlane((uint32_t)t, 0) & kM;
-        cy = t >> kBits;
-        A0 = (uint64_t)(wnext((uint32_t)t) & mv);
-        m2 = m1;
-        m1 = m;
-      } else {
-        const uint32_t m = __builtin_amdgcn_readlane((uint32_t)A0, 0) & kM;
-        acc[(r + 1) % kLL] += A0 >> kBits;
-        A0 = (uint64_t)(wnext((uint32_t)A0) & mv);
-        m2 = m1;
-        m1 = m;
-      }
+      const uint32_t m = __builtin_amdgcn_readlane((uint32_t)A0, 0) & kM;
+      acc[(r + 1) % kLL] += A0 >> kBits;
+      A0 = (uint64_t)(wnext((uint32_t)A0) & mv);
+      m2 = m1;
+      m1 = m;
     }
   }
-  if constexpr (CYL) acc[0] += cy;  // 144 = 48 x 3 steps: the next retiring column is acc[0]
   // the last two digits: after 144 steps position P holds column 144 + P, m_142 * p~_J belongs to
   // P = J - 2 (pd) and m_143 * p~_J to P = J - 1 (pd1)
 #pragma unroll
@@ -271,12 +252,11 @@ __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[k
   for (int j = 0; j < kLL; ++j) x[j] = ((uint32_t)d[j] & kM) + (j == 0 ? c_in : (uint32_t)(d[j - 1] >> kBits));
 }
 
-// MODE 0: general p, 1: p = -1 mod 2^29 (n0 = 1), 2: p = -1 mod 2^58 (delayed quotient, mul_d2),
-// 3: MODE 2 with the carry added last (mul_d2<true>)
+// MODE 0: general p, 1: p = -1 mod 2^29 (n0 = 1), 2: p = -1 mod 2^58 (delayed quotient, mul_d2)
 template <int MODE>
 __device__ __forceinline__ void mulm(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&p)[kLL],
                                      const uint32_t (&pd)[kLL], const uint32_t (&pd1)[kLL], uint32_t n0, uint32_t mv) {
-  if constexpr (MODE >= 2) mul_d2<MODE == 3>(x, y, pd, pd1, mv);
+  if constexpr (MODE == 2) mul_d2(x, y, pd, pd1, mv);
   else mul<MODE == 1>(x, y, p, n0, mv);
 }
 
@@ -562,8 +542,8 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
 #pragma unroll
   for (int j = 0; j < kLL; ++j) {
     p[j] = C->p[kLL * ln + j];
-    pd[j] = MODE >= 2 ? C->pd[kLL * ln + j] : 0u;
-    pd1[j] = MODE >= 2 ? C->pd1[kLL * ln + j] : 0u;
+    pd[j] = MODE == 2 ? C->pd[kLL * ln + j] : 0u;
+    pd1[j] = MODE == 2 ? C->pd1[kLL * ln + j] : 0u;
   }
   if (wv == 0) {
     const uint32_t rows[3] = {J.exp, J.fexp[0], J.fexp[1]};
@@ -698,316 +678,9 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
 }
 }  // namespace egw
 
-// =================================================================================================
-// Three waves per Montgomery multiply (egc): the latency shape for one job per CU.  One wave (egw)
-// runs a CIOS step of a 144-limb multiply as 6 MACs + ~5 other VALU on 48 lanes x 3 limbs, and a
-// lone wave issues at half rate, so a step costs ~87 cycles.  Here limb L = 48 w + l of an element is
-// lane l of wave w of a group of three: a step is 2 MACs (x_L y_i and the quotient term) + the
-// carry split and shift (3 VALU) + one LDS word, the waves of the group run side by side on three
-// SIMDs, and they meet every 8 steps:
-//   * y (the multiplier) is a 144-limb vector in LDS; every lane reads y_i as a broadcast (four at a
-//     time) straight into the MAC;
-//   * the quotient digit m_i = (column i) mod 2^29 appears in lane 0 of wave 0 and is applied 8 steps
-//     late (p + 1 = 0 mod 2^232: the products m_i (p + 1)_k, k >= 8, all land at or above column
-//     i + 8; position L takes m_(i-8) (p + 1)_(L+8)), through a 16-word LDS ring, so no wave waits on
-//     another within a group of 8 steps;
-//   * the low limb that leaves lane 0 of wave w + 1 at each step belongs to lane 47 of wave w: wave
-//     w + 1 leaves it in an LDS ring and wave w adds it, 8 steps later, to the lane it has moved to
-//     (lanes 40..47 at the group's end; the sum is the same, the column is 40+ steps from retiring);
-//   * the two closing carry passes exchange lane 47's carry through LDS.
-// A job's workgroup holds two groups (6 waves): group A squares the chain x^(2^i), group B multiplies
-// the set bits' powers in from an LDS ring, a slot (one multiply each) behind, and takes a fixed-base
-// window in slots whose bit is clear; the groups run in lockstep (every barrier is the workgroup's),
-// a group with nothing to do keeps the barriers.  The result is egw's integer, exported by wave 0.
-// =================================================================================================
-namespace egc {
-using egw::kBits;
-using egw::kLanes;
-using egw::kLimbs;
-using egw::kLL;
-using egw::kM;
-using egw::kRow;
-constexpr int kGW = 3;      // waves per multiply group
-constexpr int kGrp = 8;     // steps between two barriers (= the quotient delay)
-constexpr int kTrash = 17;  // words per lane of the write-off area (odd stride: no two lanes share a bank)
-
-struct Group {
-  uint32_t out[kGW][16];  // lane 0's low limb per step: wave 0 the quotient digits, waves 1-2 the boundary
-  uint32_t cy[kGW][4];    // the closing carry passes: lane 47's carry (pass 1 lo, hi; pass 2)
-};
-
-// x <- x * y * R^-1 mod p (result < 2p, limbs < 2^29 + 2^8) for the element of this wave's group;
-// s_y: 144 limbs (16-byte aligned, 4 readable words past the end); every wave of the workgroup calls it
-// together (the barriers are the workgroup's); active = false keeps only the barriers.
-__device__ __forceinline__ void mm(uint32_t& x, const uint32_t* __restrict__ s_y, const uint32_t (&pk)[8], Group& G,
-                                   uint32_t* __restrict__ trash, uint32_t gw, uint32_t l, uint32_t mv, bool active) {
-  uint64_t A = 0;
-  uint32_t* wr = l == 0 ? &G.out[gw][0] : trash + kTrash * l;  // lane 0: the ring; the rest: write-off words
-  uint32_t inj = 0;  // the boundary word this lane adds at the end of the group (issued after the barrier)
-#pragma unroll 1
-  for (int g = 0; g < kLimbs / kGrp; ++g) {
-    if (active) {
-      // m_(i-8) for the group's steps (group 0 reads slots 8..15, which hold zeros between multiplies)
-      uint4 mq[2];
-      mq[0] = *reinterpret_cast<const uint4*>(&G.out[0][(kGrp * g - kGrp) & 15]);
-      mq[1] = *reinterpret_cast<const uint4*>(&G.out[0][(kGrp * g - kGrp + 4) & 15]);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint4 y4 = *reinterpret_cast<const uint4*>(s_y + kGrp * g + 4 * h);
-        const uint32_t ys[4] = {y4.x, y4.y, y4.z, y4.w};
-        const uint32_t ms[4] = {mq[h].x, mq[h].y, mq[h].z, mq[h].w};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          A = (uint64_t)x * ys[s] + A;
-          A = (uint64_t)pk[7] * ms[s] + A;
-          wr[(4 * h + s + (g & 1) * kGrp)] = (uint32_t)A & kM;  // step i = 8 g + 4 h + s: slot i & 15
-          const uint64_t c = A >> kBits;
-          A = (uint64_t)(egw::wnext((uint32_t)A) & mv) + c;
-        }
-      }
-      // the word wave w + 1 left at step 8 (g - 1) + j has moved to lane 32 + j (0 in group 0)
-      A = (uint64_t)inj * 1u + A;
-    }
-    __syncthreads();
-    if (active) {
-      inj = 0;
-      if (gw + 1 < (uint32_t)kGW && l >= 32 && l < 40) inj = G.out[gw + 1][(kGrp * g + (l - 32)) & 15];
-    }
-  }
-  if (active) {
-    // the last group's words sit in lanes 40..47 now
-    if (gw + 1 < (uint32_t)kGW && l >= 40 && l < 48) A += G.out[gw + 1][((kLimbs - kGrp) + (l - 40)) & 15];
-    // the last 8 digits: m_(136+t) (p + 1)_(P + 8 - t) at position P
-    const uint4 ma = *reinterpret_cast<const uint4*>(&G.out[0][(kLimbs - 8) & 15]);
-    const uint4 mb = *reinterpret_cast<const uint4*>(&G.out[0][(kLimbs - 4) & 15]);
-    A = (uint64_t)pk[7] * ma.x + A;
-    A = (uint64_t)pk[6] * ma.y + A;
-    A = (uint64_t)pk[5] * ma.z + A;
-    A = (uint64_t)pk[4] * ma.w + A;
-    A = (uint64_t)pk[3] * mb.x + A;
-    A = (uint64_t)pk[2] * mb.y + A;
-    A = (uint64_t)pk[1] * mb.z + A;
-    A = (uint64_t)pk[0] * mb.w + A;
-  }
-  // two carry passes; lane 47's carry crosses to the next wave's lane 0 through LDS
-  const uint64_t c1 = A >> kBits;
-  if (active && l == kLanes - 1) {
-    G.cy[gw][0] = (uint32_t)c1;
-    G.cy[gw][1] = (uint32_t)(c1 >> 32);
-  }
-  uint64_t cin = (uint64_t)egw::wprev((uint32_t)c1) | ((uint64_t)egw::wprev((uint32_t)(c1 >> 32)) << 32);
-  __syncthreads();
-  // every read of the digit ring is done: slots 8..15 go back to zero for the next multiply's group 0
-  if (active && gw == 0 && l < 8) G.out[0][8 + l] = 0u;
-  if (gw > 0 && l == 0) cin = (uint64_t)G.cy[gw - 1][0] | ((uint64_t)G.cy[gw - 1][1] << 32);
-  const uint64_t d = (uint64_t)((uint32_t)A & kM) + cin;
-  const uint32_t c2 = (uint32_t)(d >> kBits);
-  if (active && l == kLanes - 1) G.cy[gw][2] = c2;
-  uint32_t cin2 = egw::wprev(c2);
-  __syncthreads();
-  if (gw > 0 && l == 0) cin2 = G.cy[gw - 1][2];
-  if (active) x = l < (uint32_t)kLanes ? ((uint32_t)d & kM) + cin2 : 0u;
-}
-
-// One job per workgroup of 6 waves (2 groups of 3): out = (prod bases)^exp * T0^f0 * T1^f1 mod p, as
-// egw::k_wave_job (WaveJob, WaveTab, the same integer), variable time only.
-__global__ void __launch_bounds__(64 * 2 * kGW) k_coop_job(const egw::Consts* __restrict__ C,
-                                                           const WaveJob* __restrict__ jobs, uint32_t njobs,
-                                                           const WaveTab* __restrict__ tabs,
-                                                           const uint8_t* __restrict__ bases,
-                                                           const uint8_t* __restrict__ exps, uint8_t* __restrict__ out_be) {
-  __shared__ __align__(16) uint32_t s_ring[2][kRow];   // the chain's powers, two slots
-  __shared__ __align__(16) uint32_t s_stage[2][kRow];  // per group: the staged multiplier (table entry, base)
-  __shared__ __align__(16) uint32_t s_r2[kRow];        // R^2 mod p
-  __shared__ __align__(16) uint32_t s_unit[kRow];      // 1
-  __shared__ uint32_t s_w[kRow];                       // egw byte <-> limb staging (wave 0)
-  __shared__ uint32_t s_x[3][9];                       // the exponents (variable, fixed 0, fixed 1)
-  __shared__ __align__(16) Group s_grp[2];
-  __shared__ uint32_t s_trash[kTrash * 64];
-  const uint32_t e = blockIdx.x;
-  if (e >= njobs) return;
-  const WaveJob J = jobs[e];
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t grp = wv / kGW, gw = wv % kGW, l = egw::lane64();
-  const uint32_t L = kLanes * gw + l;
-  const bool live = l < (uint32_t)kLanes;
-  uint32_t mv;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(mv) : "s"(C->mask));
-  uint32_t pk[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) pk[k] = live ? C->pk[k][L] : 0u;
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kRow; i += blockDim.x) {
-    s_r2[i] = i < (uint32_t)kLimbs ? C->r2[i] : 0u;
-    s_unit[i] = i == 0 ? 1u : 0u;
-  }
-  if (threadIdx.x < 2 * 16) s_grp[threadIdx.x >> 4].out[0][threadIdx.x & 15] = 0u;  // the digit rings
-  if (wv == 0) {
-    const uint32_t rows[3] = {J.exp, J.fexp[0], J.fexp[1]};
-    if (l < 24) {
-      const uint32_t sl = l >> 3, w = l & 7u, r = rows[sl];
-      const bool used = r != kWaveNone && (sl == 0 || J.tab[sl - 1] != kWaveNone);
-      s_x[sl][7 - w] = used ? __builtin_bswap32(reinterpret_cast<const uint32_t*>(exps + (size_t)r * 32)[w]) : 0u;
-    }
-    if (l < 3) s_x[l][8] = 0u;
-  }
-  const WaveTab T0 = J.tab[0] != kWaveNone ? tabs[J.tab[0]] : WaveTab{nullptr, 0, 0};
-  const WaveTab T1 = J.tab[1] != kWaveNone ? tabs[J.tab[1]] : WaveTab{nullptr, 0, 0};
-  const uint32_t nw0 = J.tab[0] != kWaveNone ? T0.nwin : 0u, nw = nw0 + (J.tab[1] != kWaveNone ? T1.nwin : 0u);
-  __syncthreads();  // s_x, s_r2, s_unit
-  Group& G = s_grp[grp];
-  uint32_t x = 0;         // this group's accumulator (a limb per lane)
-  bool started = false;   // ... holds a factor
-  // the fixed-base window kk's digit (0: skip) and its entry staged as this group's multiplier
-  auto window_digit = [&](uint32_t kk) -> uint32_t {
-    const bool second = kk >= nw0;
-    const WaveTab& T = second ? T1 : T0;
-    const uint32_t k = second ? kk - nw0 : kk;
-    return egw::exp_digit(s_x[second ? 2 : 1], k * T.wbits, T.wbits);
-  };
-  auto stage_window = [&](uint32_t kk, uint32_t dg) {
-    const bool second = kk >= nw0;
-    const WaveTab& T = second ? T1 : T0;
-    const uint32_t k = second ? kk - nw0 : kk;
-    const uint32_t* ent = T.data + (((size_t)k << T.wbits) + dg) * 160;
-    if (live) s_stage[grp][L] = ent[(L / 18) * 20 + L % 18];
-  };
-  // the next window with a nonzero digit at or after kk (nw: none)
-  auto next_window = [&](uint32_t kk) -> uint32_t {
-    while (kk < nw && window_digit(kk) == 0) ++kk;
-    return kk;
-  };
-  // x <- x * s (or x <- s when this group holds nothing yet): the copy needs no multiply
-  auto take = [&](const uint32_t* s_src, bool act) {
-    if (act && !started && live) x = s_src[L];
-    mm(x, s_src, pk, G, s_trash, gw, l, mv, act && started);
-    if (act) started = true;
-  };
-  const bool has_var = J.nbase > 0;
-  // 1. the variable part's base: the product of the job's bases in the Montgomery domain (group A)
-  if (has_var) {
-#pragma unroll 1
-    for (uint32_t k = 0; k < J.nbase; ++k) {
-      // wave 0 imports the base (egw layout) and spreads its limbs through s_stage[0]
-      if (wv == 0) {
-        uint32_t y3[kLL];
-        egw::import_be(bases + (size_t)(J.base + k) * 512, y3, s_w, l);
-#pragma unroll
-        for (int j = 0; j < kLL; ++j)
-          if (live) s_stage[0][kLL * l + j] = y3[j];
-      }
-      __syncthreads();
-      uint32_t b = (grp == 0 && live) ? s_stage[0][L] : 0u;
-      mm(b, s_r2, pk, G, s_trash, gw, l, mv, grp == 0);  // b R (the Montgomery domain)
-      if (k == 0) {
-        if (grp == 0) x = b;
-        __syncthreads();
-      } else {
-        if (grp == 0 && live) s_stage[0][L] = b;
-        __syncthreads();
-        mm(x, s_stage[0], pk, G, s_trash, gw, l, mv, grp == 0);
-      }
-    }
-    if (grp == 0) started = true;
-  }
-  // 2. the exponent, right to left: slot s: A squares P_(s-1) -> P_s, B multiplies P_(s-1) in when bit
-  //    s - 1 is set, else takes its next fixed-base window
-  uint32_t kk = next_window(0);  // the next fixed-base window (both groups walk the same list)
-  if (has_var && J.exp != kWaveNone) {
-    auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_x[0][i >> 5]) >> (i & 31)) & 1u; };
-    int top = 255;
-    while (top >= 0 && !bit(top)) --top;
-    if (grp == 0 && live) s_ring[0][L] = x;  // P_0
-    const bool a_var = grp == 0;
-    bool b_fixed = false;  // B took window kk this slot
-    uint32_t b_dg = 0;
-    // B's slot 1: bit 0, or a window
-    if (top >= 0 && !bit(0) && kk < nw) {
-      b_dg = window_digit(kk);
-      if (grp == 1) stage_window(kk, b_dg);
-      b_fixed = true;
-    }
-    __syncthreads();
-    if (grp == 0) started = false;  // A's chain is not a factor
-#pragma unroll 1
-    for (int sl = 1; sl <= top + 1; ++sl) {
-      const uint32_t* prev = s_ring[(sl - 1) & 1];
-      // A: P_sl = P_(sl-1)^2 (up to the top bit)
-      // B: bit sl - 1 -> x_B *= P_(sl-1); else the staged window
-      const bool a_act = a_var && sl <= top;
-      const bool b_bit = bit(sl - 1) != 0;
-      if (grp == 0) {
-        if (a_act) mm(x, prev, pk, G, s_trash, gw, l, mv, true);
-        else mm(x, prev, pk, G, s_trash, gw, l, mv, false);
-      } else {
-        if (b_bit) take(prev, true);
-        else if (b_fixed) take(s_stage[1], true);
-        else mm(x, prev, pk, G, s_trash, gw, l, mv, false);
-      }
-      if (!b_bit && b_fixed) kk = next_window(kk + 1);
-      // the next slot: A's power into the ring, B's window staged when the next bit is clear
-      if (grp == 0 && a_act && live) s_ring[sl & 1][L] = x;
-      b_fixed = false;
-      if (sl <= top && !bit(sl) && kk < nw) {
-        b_dg = window_digit(kk);
-        if (grp == 1) stage_window(kk, b_dg);
-        b_fixed = true;
-      }
-      __syncthreads();
-    }
-  }
-  // 3. the remaining fixed-base windows, alternately on A and B
-#pragma unroll 1
-  while (kk < nw) {
-    const uint32_t ka = kk, kb = next_window(kk + 1);
-    const bool hb = kb < nw;
-    if (grp == 0) stage_window(ka, window_digit(ka));
-    if (grp == 1 && hb) stage_window(kb, window_digit(kb));
-    __syncthreads();
-    if (grp == 0) take(s_stage[0], true);
-    else if (hb) take(s_stage[1], true);
-    else mm(x, s_stage[1], pk, G, s_trash, gw, l, mv, false);
-    kk = hb ? next_window(kb + 1) : nw;
-    __syncthreads();
-  }
-  // 4. A <- A * B; leave the Montgomery domain; wave 0 exports
-  __shared__ uint32_t s_has[2];
-  if (l == 0 && gw == 0) s_has[grp] = started ? 1u : 0u;
-  __syncthreads();
-  const bool ha = s_has[0] != 0, hb = s_has[1] != 0;
-  if (grp == 1 && hb && live) s_stage[1][L] = x;
-  __syncthreads();
-  if (grp == 0) {
-    if (ha && hb) {
-      mm(x, s_stage[1], pk, G, s_trash, gw, l, mv, true);
-    } else {
-      if (!ha && hb && live) x = s_stage[1][L];
-      if (!ha && !hb && live) x = C->one[L];
-      mm(x, s_stage[1], pk, G, s_trash, gw, l, mv, false);
-    }
-  } else {
-    mm(x, s_stage[1], pk, G, s_trash, gw, l, mv, false);
-  }
-  mm(x, s_unit, pk, G, s_trash, gw, l, mv, grp == 0);  // x R^-1: a value in [0, p]
-  if (grp == 0 && live) s_stage[0][L] = x;
-  __syncthreads();
-  if (wv == 0) {
-    uint32_t x3[kLL], p3[kLL];
-#pragma unroll
-    for (int j = 0; j < kLL; ++j) {
-      x3[j] = live ? s_stage[0][kLL * l + j] : 0u;
-      p3[j] = C->p[kLL * l + j];
-    }
-    egw::normalize(x3, p3, l);
-    egw::export_be(x3, out_be + (size_t)J.out * 512, s_w, l);
-  }
-}
-}  // namespace egc
-
 struct PowWaveConsts {
   egw::Consts* d = nullptr;
   bool d2 = false;  // p = -1 mod 2^58: the delayed-quotient multiply (EG_POWWAVE_D2=0 keeps mul<true>)
-  bool cyl = false;  // ... with the carry added last (EG_POWWAVE_CYL=1; A/B)
-  bool coop = false;  // p + 1 = 0 mod 2^232: the three-wave multiply for one-job-per-CU batches (EG_COOP=1)
 };
 
 int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t* one, uint32_t n0, uint32_t friendly,
@@ -1028,7 +701,6 @@ int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t*
   limbs(p, 128, h.p);
   limbs(r2, 129, h.r2);
   limbs(one, 129, h.one);
-  bool d8 = true;  // p + 1 = 0 mod 2^232 (the three-wave multiply's quotient delay)
   // p + 1 (129 words: the carry out of the top word is zero for p < 2^4096 - 1) in limbs, shifted down
   // by two and by one limb for the delayed-quotient multiply
   {
@@ -1046,21 +718,14 @@ int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t*
     for (int a = 0; a < egw::kRow; ++a) {
       h.pd[a] = a + 2 < egw::kLimbs ? pt[a + 2] : 0u;
       h.pd1[a] = a + 1 < egw::kLimbs ? pt[a + 1] : 0u;
-      for (int k = 0; k < 8; ++k) h.pk[k][a] = a + k + 1 < egw::kLimbs ? pt[a + k + 1] : 0u;
     }
-    // the three-wave multiply delays each quotient digit by 8 steps: p + 1 = 0 mod 2^232 (limbs 0-7)
-    for (int a = 0; a < 8; ++a) d8 &= pt[a] == 0u;
   }
   h.n0 = n0;
   h.mask = egw::kM;
   auto* c = new PowWaveConsts();
   {
-    const char* co = std::getenv("EG_COOP");
-    c->coop = d8 && co && co[0] == '1';
     const char* env = std::getenv("EG_POWWAVE_D2");
     c->d2 = p[0] == 0xFFFFFFFFu && (p[1] & 0x03FFFFFFu) == 0x03FFFFFFu && !(env && env[0] == '0');
-    const char* cy = std::getenv("EG_POWWAVE_CYL");
-    c->cyl = cy && cy[0] == '1';
   }
   hipError_t e = hipMalloc(&c->d, sizeof(egw::Consts));
   if (e == hipSuccess) e = hipMemcpy(c->d, &h, sizeof(egw::Consts), hipMemcpyHostToDevice);
@@ -1105,15 +770,13 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool
     else                     \
       EGW_LAUNCH(M, CTV, 1); \
   } while (0)
-  const int mode = (friendly && C->d2) ? (C->cyl ? 3 : 2) : (friendly ? 1 : 0);
+  const int mode = (friendly && C->d2) ? 2 : (friendly ? 1 : 0);
   if (ct) {
-    if (mode == 3) EGW_LAUNCH_W(3, true);
-    else if (mode == 2) EGW_LAUNCH_W(2, true);
+    if (mode == 2) EGW_LAUNCH_W(2, true);
     else if (mode == 1) EGW_LAUNCH_W(1, true);
     else EGW_LAUNCH_W(0, true);
   } else {
-    if (mode == 3) EGW_LAUNCH_W(3, false);
-    else if (mode == 2) EGW_LAUNCH_W(2, false);
+    if (mode == 2) EGW_LAUNCH_W(2, false);
     else if (mode == 1) EGW_LAUNCH_W(1, false);
     else EGW_LAUNCH_W(0, false);
   }
@@ -1122,25 +785,6 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     *err = std::string("powwave launch: ") + hipGetErrorString(e);
-    return 1;
-  }
-  return 0;
-}
-
-bool powwave_coop(const PowWaveConsts* C) { return C && C->coop; }
-
-int powwave_coop_jobs(const PowWaveConsts* C, hipStream_t s, const WaveJob* d_jobs, uint32_t njobs, const WaveTab* d_tabs,
-                      const uint8_t* d_bases, const uint8_t* d_exps, uint8_t* d_out, std::string* err) {
-  if (!njobs) return 0;
-  if (!C->coop) {
-    *err = "powwave: the three-wave multiply needs p + 1 = 0 mod 2^232";
-    return 1;
-  }
-  hipLaunchKernelGGL(egc::k_coop_job, dim3(njobs), dim3(64 * 2 * egc::kGW), 0, s, C->d, d_jobs, njobs, d_tabs, d_bases,
-                     d_exps, d_out);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    *err = std::string("coop launch: ") + hipGetErrorString(e);
     return 1;
   }
   return 0;

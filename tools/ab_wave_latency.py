@@ -1,6 +1,6 @@
 """Latency of one per-element exponentiation on the per-wave kernel (the shape upstream's per-element
 callers wait on), for the A/Bs of its multiply variants (env read at context creation, e.g.
-EG_POWWAVE_CYL=0, EG_WAVE_R2L=0, EG_POWWAVE_D2=0).  Every result is checked against CPython.
+EG_WAVE_R2L=0, EG_POWWAVE_D2=0).  Every result is checked against CPython.
 
     python tools/ab_wave_latency.py [calls=200]
 Prints one JSON line: blocking powP (eg_powp_one, one thread), a one-element eg_powp_batch, and a

@@ -67,9 +67,8 @@ if [[ $STEPS == *abw4* ]]; then
   echo "abw4: $(tail -c 900 gpurun_out/${TAG}_ab_w4.log)"
 fi
 if [[ $STEPS == *lat* ]]; then
-  # per-wave latency A/B: carry-last delayed-quotient multiply against carry-first, right to left
-  # against one wave (tools/ab_wave_latency.py), interleaved
-  IFS=';' read -ra LE <<< "${LAT_ENVS:-EG_COOP=1;EG_COOP=0 EG_POWWAVE_CYL=1;EG_COOP=0}"
+  # per-wave latency A/B (tools/ab_wave_latency.py), interleaved; LAT_ENVS: ';'-separated env sets
+  IFS=';' read -ra LE <<< "${LAT_ENVS:-EG_WAVE_R2L=256;EG_WAVE_R2L=0}"
   for r in $(seq ${LAT_ROUNDS:-2}); do
     for envs in "${LE[@]}"; do
       env $envs timeout -k 10 ${LAT_TIMEOUT:-300} python tools/ab_wave_latency.py ${LAT_CALLS:-200} >> gpurun_out/${TAG}_wave_latency.jsonl \
