@@ -77,3 +77,12 @@ if [[ $STEPS == *lat* ]]; then
   done
   echo "lat: $(cat gpurun_out/${TAG}_wave_latency.jsonl)"
 fi
+if [[ $STEPS == *evid* ]]; then
+  # configs[4] full pipeline at one GPU's 125,000-ballot share; the N = 2 launcher shape at configs[2]'s
+  # full per-rank shard (125,000 ballots per rank) over gloo, both ranks on this one MI355X
+  timeout -k 10 600 python bench.py --pipeline full > gpurun_out/${TAG}_bench_pipeline_config4.log 2>&1
+  echo "pipe: $(tail -c 300 gpurun_out/${TAG}_bench_pipeline_config4.log)"
+  timeout -k 10 600 env EG_DIST_BACKEND=gloo python bench.py --gpus 2 --ballots 125000 --steps 2 --warmup 1 \
+    > gpurun_out/${TAG}_rehearse_gloo2_config2_full.log 2>&1
+  echo "gloo2: $(tail -c 300 gpurun_out/${TAG}_rehearse_gloo2_config2_full.log)"
+fi
