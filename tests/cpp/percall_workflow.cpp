@@ -48,6 +48,8 @@ int ego_encrypt_ballots(const uint8_t qbar[32], size_t nb, size_t nc, size_t spc
 int ego_verify_ballots(const uint8_t qbar[32], size_t nb, size_t nc, size_t spc, size_t ph, uint32_t limit,
                        const uint8_t* cts, const uint8_t* rproof, const uint8_t* cproof, uint8_t* ok_sel,
                        uint8_t* ok_con, uint8_t* tally, int threads);
+int ego_trustee_decrypt(const uint8_t secret[32], const uint8_t qbar[32], const uint8_t* texts, const uint8_t* nonces,
+                        size_t n, uint8_t* out_M, uint8_t* out_proof, int threads);
 }
 
 using namespace electionguard;
@@ -302,17 +304,50 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < accs.size(); ++i) std::memcpy(&tal[i * 512], accs[i].byteArray(), 512);
     const double gt = secs(t);
     const long tal_mis = tal != tal_ref;
+    // ---- a trustee's direct decryption shares (DecryptingTrustee.directDecrypt: one thread over the
+    //      texts, RunRemoteDecryptingTrustee.java:189-193) through the per-element API with the
+    //      constant-time schedules (the secret exponent), against the port on one thread ----
+    const size_t nt = std::min<size_t>(nb * kNSEL, 1100);
+    const ElementModQ sk = G.randomElementModQ(rng);
+    std::vector<uint8_t> tn(nt * 32), tM_ref(nt * 512), tP_ref(nt * 64), tM(nt * 512), tP(nt * 64);
+    for (size_t i = 0; i < nt; ++i) G.randomElementModQ(rng).v.to_be(&tn[i * 32]);
+    const auto skb = sk.byteArray();
+    t = Clock::now();
+    ego_trustee_decrypt(skb.data(), qbar.data(), cts_ref.data(), tn.data(), nt, tM_ref.data(), tP_ref.data(), 1);
+    const double tr_cpu = secs(t);
+    G.setConstantTime(true);
+    auto share = [&](size_t i, uint8_t* M_out, uint8_t* P_out) {
+      const ElementModP pad = G.binaryToElementModP(&cts_ref[i * 1024]), dat = G.binaryToElementModP(&cts_ref[i * 1024 + 512]);
+      const ElementModQ u = q_at(&tn[i * 32]);
+      const ElementModP M = pad.powP(sk), a = G.gPowP(u), b = pad.powP(u);
+      const ElementModQ c = hashElements(G, E.qbar, {&pad, &dat, &a, &b, &M});
+      const ElementModQ v = G.subQ(u, G.mulQ(c, sk));
+      std::memcpy(M_out, M.byteArray(), 512);
+      c.v.to_be(P_out);
+      v.v.to_be(P_out + 32);
+    };
+    {
+      uint8_t m1[512], p1[64];
+      share(0, m1, p1);  // warm-up: the constant-time companion of g's table
+    }
+    t = Clock::now();
+    for (size_t i = 0; i < nt; ++i) share(i, &tM[i * 512], &tP[i * 64]);
+    const double tr_gpu = secs(t);
+    G.setConstantTime(ct);
+    const long tr_mis = (long)(tM != tM_ref) + (long)(tP != tP_ref);
     printf("{\"ballots\": %zu, \"threads\": %d, \"deferred\": %s, \"constant_time\": %s, \"selections_per_ballot\": %zu, "
            "\"encrypt_mismatched_arrays\": %ld, \"verify_flag_mismatches\": %ld, \"invalid_flags\": %ld, "
            "\"tamper_not_rejected\": %ld, \"tally_mismatch\": %ld, \"errors\": %ld, "
            "\"encrypt_ballots_per_s\": {\"gpu_per_element\": %.1f, \"cpu_port\": %.1f}, "
            "\"verify_ballots_per_s\": {\"gpu_per_element\": %.1f, \"cpu_port\": %.1f}, "
            "\"tally_ballots_per_s_one_thread\": {\"gpu_per_element\": %.1f, \"cpu_port\": %.1f}, "
+           "\"trustee_texts\": %zu, \"trustee_mismatched_arrays\": %ld, "
+           "\"trustee_shares_per_s_one_thread\": {\"gpu_per_element_constant_time\": %.1f, \"cpu_port\": %.1f}, "
            "\"cpu_port\": \"oracle/eg_oracle_c.c (OpenSSL BN_mod_exp_mont + 8-bit radix fixed base), %d threads; tally: "
            "BN_mod_mul loop, one thread\"}\n",
            nb, T, eager ? "false" : "true", ct ? "true" : "false", kNSEL, enc_mis, ver_mis, invalid, tamper_mis, tal_mis, errors.load(), nb / gpu_enc_s, nb / cpu_enc_s,
-           nb / gpu_ver_s, nb / cpu_ver_s, nb / gt, nb / dt, T);
-    bad = enc_mis + ver_mis + invalid + tamper_mis + tal_mis + errors.load();
+           nb / gpu_ver_s, nb / cpu_ver_s, nb / gt, nb / dt, nt, tr_mis, nt / tr_gpu, nt / tr_cpu, T);
+    bad = enc_mis + ver_mis + invalid + tamper_mis + tal_mis + tr_mis + errors.load();
   }
   return bad == 0 ? 0 : 1;
 }

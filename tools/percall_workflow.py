@@ -54,6 +54,9 @@ def main():
                                           d["verify_ballots_per_s"]["cpu_port"], 3),
         "tally_gpu_over_cpu_port": round(d["tally_ballots_per_s_one_thread"]["gpu_per_element"] /
                                          d["tally_ballots_per_s_one_thread"]["cpu_port"], 3),
+        "trustee_gpu_ct_over_cpu_port_one_thread": round(
+            d["trustee_shares_per_s_one_thread"]["gpu_per_element_constant_time"] /
+            d["trustee_shares_per_s_one_thread"]["cpu_port"], 3),
         "verify_r2l_over_one_wave_best": round(best("deferred", "verify_ballots_per_s") /
                                                best("deferred_var_one_wave", "verify_ballots_per_s"), 3),
         "encrypt_r2l_over_one_wave_best": round(best("deferred", "encrypt_ballots_per_s") /
