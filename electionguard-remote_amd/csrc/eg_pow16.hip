@@ -202,15 +202,24 @@ __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL]
 // MAC -> carry shift -> add, the readlane of the quotient runs beside it.  The quotient digits are the
 // standard CIOS ones (the m-terms of columns < i + 8 telescope to multiples of 2^29 for this p), so
 // the result is the same integer as mul<true>.  The last two digits are applied after the loop.
+// The multiplier's digits reach the MACs as LDS broadcasts (the wave's own copy of y, read a trip
+// ahead, two register sets in turn) instead of one v_readlane per step.
 __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&pd)[kLL],
                                        const uint32_t (&pd1)[kLL], uint32_t mv) {
+  __shared__ __align__(16) uint32_t s_yb[4][kRow + 8];  // per wave of the workgroup (W <= 4)
+  uint32_t* yb = s_yb[threadIdx.x >> 6];
+  const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  __builtin_amdgcn_wave_barrier();  // the previous multiply's reads of yb are done (in-order LDS)
+#pragma unroll
+  for (int j = 0; j < kLL; ++j) yb[kLL * ln + j] = y[j];
+  __builtin_amdgcn_wave_barrier();
   uint64_t acc[kLL] = {0, 0, 0};
   uint32_t m1 = 0, m2 = 0;  // quotient digits of the previous two steps
-#pragma unroll 1
-  for (int q = 0; q < kLanes; ++q) {
+  // three CIOS steps with the multiplier digits yc (limbs 3q .. 3q + 2)
+  auto steps = [&](const uint32_t (&yc)[kLL]) {
 #pragma unroll
     for (int r = 0; r < kLL; ++r) {
-      const uint32_t yi = __builtin_amdgcn_readlane(y[r], q);
+      const uint32_t yi = yc[r];
 #pragma unroll
       for (int j = 0; j < kLL; ++j) {
         uint64_t& A = acc[(j + r) % kLL];
@@ -233,6 +242,21 @@ __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[k
       m2 = m1;
       m1 = m;
     }
+  };
+  uint32_t ya[kLL] = {yb[0], yb[1], yb[2]}, yz[kLL];
+#pragma unroll 1
+  for (int q = 0; q < kLanes; q += 2) {
+    const uint32_t* yq = yb + kLL * q;
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) yz[r] = yq[kLL + r];  // trip q + 1's digits
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) asm volatile("" : "+v"(ya[r]));  // VGPR operands (no readfirstlane)
+    steps(ya);
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) ya[r] = yq[2 * kLL + r];  // trip q + 2's (yb[144..146]: 0)
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) asm volatile("" : "+v"(yz[r]));
+    steps(yz);
   }
   // the last two digits: after 144 steps position P holds column 144 + P, m_142 * p~_J belongs to
   // P = J - 2 (pd) and m_143 * p~_J to P = J - 1 (pd1)
