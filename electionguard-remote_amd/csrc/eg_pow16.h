@@ -61,13 +61,13 @@ struct WaveJob {
 // variable-base term, masked scans of every window column and no zero-digit skip for fixed-base terms,
 // whose tables must then have wbits <= 8).
 // waves > 1: four waves per job, the fixed-base windows split over them (eg_pow16.hip k_wave_job); with
-// r2l (variable time only) the variable part runs right to left over the four waves too (the latency
-// shape for batches of at most one job per CU).
+// r2l the variable part runs right to left over the four waves too (the latency shape for batches of at
+// most one job per CU; with ct its constant-time schedule).
 int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool r2l, hipStream_t s,
                  const WaveJob* d_jobs, WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident,
                  const uint8_t* d_bases, const uint8_t* d_exps, uint8_t* d_out, std::string* err);
 // out_be[i] = base_be[i]^exp_be[i] mod p (device pointers, asynchronous on s; no scratch); r2l: four
-// waves per element, right to left (ignored with ct)
+// waves per element, right to left
 int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, bool r2l, hipStream_t s, const uint8_t* base_be,
                  const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err);
 // out_be[i] = base^exp_be[i] mod p over a fixed-base radix table, one element per wave

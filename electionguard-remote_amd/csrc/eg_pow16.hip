@@ -525,14 +525,17 @@ __device__ __forceinline__ void pow_fixed(uint32_t (&x)[kLL], bool& started, con
 // LDS and fold in a log2(W) tree: a fixed-base term of n windows costs ~n/W + log2(W) multiplies of
 // latency instead of n.  jobs == nullptr: job e is `dflt` with its rows offset by e (the batch entry
 // points: element e of every input array).
-// r2l (W > 1, variable time, a job with an exponent): the variable part runs right to left instead.
+// r2l (W > 1, a job with an exponent): the variable part runs right to left instead.
 // Wave 0 only squares, x_i = x^(2^i) for i up to the exponent's top bit, W - 1 squarings per round,
 // and leaves each round's powers in a double-buffered LDS ring; in the next round wave k (1 <= k < W)
 // multiplies x_i with i = (round - 1)(W - 1) + k - 1 into its partial when bit i is set, then takes one
 // of its fixed-base windows.  A wave does at most 2 multiplies while wave 0 does W - 1 = 3 squarings,
 // so the chain never waits: the latency is the top bit + ~4 operations against ~16 (window table) +
 // the top bit + ~43 (window multiplies) for the left-to-right sliding window (one SIMD per wave: the
-// waves issue side by side).  The host enables it for batches of at most one job per CU.
+// waves issue side by side).  The host enables it for batches of at most one job per CU.  CT: the chain
+// runs all 255 squarings and every multiplying wave multiplies in every round, by x_i or by 1 (a
+// masked select of the two), and takes its fixed-base windows as masked scans: the same operations
+// for every exponent.
 template <int MODE, bool CT, int W>
 __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ C, const WaveJob* __restrict__ jobs,
                                                      WaveJob dflt, uint32_t njobs, const WaveTab* __restrict__ tabs,
@@ -584,7 +587,7 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
   // an exponent on an empty product: 1^e = 1 (no variable part)
   const bool has_var = J.nbase > 0;
   // right to left over W waves (wave-uniform: the same for every wave of the job)
-  const bool split = W > 1 && !CT && r2l && has_var && J.exp != kWaveNone;
+  const bool split = W > 1 && r2l && has_var && J.exp != kWaveNone;
   __syncthreads();  // s_x
   bool started = false;
   if (wv == 0 && has_var) {
@@ -607,11 +610,19 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
     }
     if (J.exp != kWaveNone && !split) pow_var<MODE, CT>(x, s_x[0], s_tab, C, p, pd, pd1, n0, mv, ln);
   }
-  if constexpr (W > 1 && !CT) {
+  if constexpr (W > 1) {
     if (split) {
       auto bit = [&](int i) -> uint32_t { return (__builtin_amdgcn_readfirstlane(s_x[0][i >> 5]) >> (i & 31)) & 1u; };
       int top = 255;
-      while (top >= 0 && !bit(top)) --top;
+      if constexpr (!CT)
+        while (top >= 0 && !bit(top)) --top;
+      if constexpr (CT) {  // every multiplying wave holds a factor from the start: 1
+        if (wv) {
+#pragma unroll
+          for (int j = 0; j < kLL; ++j) x[j] = C->one[kLL * ln + j];
+          started = true;
+        }
+      }
       constexpr int K = W - 1;
       const int rounds = top < 0 ? 0 : top / K + 1;
       const uint32_t widx = wv - 1;
@@ -631,7 +642,16 @@ __global__ void __launch_bounds__(64 * W) k_wave_job(const Consts* __restrict__ 
           }
         } else {
           const int i = (r - 1) * K + (int)widx;
-          if (r > 0 && i <= top && bit(i)) {
+          if constexpr (CT) {
+            if (r > 0 && i <= top) {  // x *= bit i ? x_i : 1, the same multiply either way
+              uint32_t msk = 0u - bit(i);
+              asm volatile("" : "+s"(msk));
+#pragma unroll
+              for (int j = 0; j < kLL; ++j)
+                y[j] = (s_ring[((r - 1) & 1) * K + widx][kLL * ln + j] & msk) | (C->one[kLL * ln + j] & ~msk);
+              mulm<MODE>(x, y, p, pd, pd1, n0, mv);
+            }
+          } else if (r > 0 && i <= top && bit(i)) {
 #pragma unroll
             for (int j = 0; j < kLL; ++j) y[j] = s_ring[((r - 1) & 1) * K + widx][kLL * ln + j];
             if (started) {
@@ -780,10 +800,10 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool
     return 1;
   }
   const dim3 grid(njobs);
-  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1); r2l (4 waves, variable
-  // time): the variable part right to left over the 4 waves
+  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1); r2l (4 waves): the
+  // variable part right to left over the 4 waves (CT: the constant-time schedule of it)
   const int W = waves > 1 ? 4 : 1;
-  const uint32_t r2l_on = (r2l && W > 1 && !ct) ? 1u : 0u;
+  const uint32_t r2l_on = (r2l && W > 1) ? 1u : 0u;
 #define EGW_LAUNCH(M, CTV, WV)                                                                                    \
   hipLaunchKernelGGL((egw::k_wave_job<M, CTV, WV>), grid, dim3(64 * WV), 0, s, C->d, d_jobs, dflt, njobs, d_tabs, \
                      d_bases, d_exps, d_out, t_ident, r2l_on)
@@ -817,7 +837,7 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool
 int powwave_powp(const PowWaveConsts* C, bool friendly, bool ct, bool r2l, hipStream_t s, const uint8_t* base_be,
                  const uint8_t* exp_be, uint8_t* out_be, size_t n, std::string* err) {
   const WaveJob d{0, 1, 0, {kWaveNone, kWaveNone}, {kWaveNone, kWaveNone}, 0};
-  const bool rl = r2l && !ct;
+  const bool rl = r2l;
   return powwave_jobs(C, friendly, ct, rl ? 4 : 1, rl, s, nullptr, d, (uint32_t)n, nullptr, WaveTab{nullptr, 0, 0},
                       base_be, exp_be, out_be, err);
 }

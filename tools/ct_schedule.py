@@ -25,7 +25,8 @@ def main():
     rng = random.Random(3)
     fb12 = G.fixed_base(pow(G.g, rng.randrange(q), G.p), 12)
     classes = {"zero": lambda: 0, "ones": lambda: 2**256 - 1, "random": lambda: rng.randrange(q)}
-    layouts = [("per-wave powP", 256), ("16-lane powP", 3000), ("8-lane powP", 9000), ("per-wave fixed-base 12-bit", 256)]
+    layouts = [("per-wave powP right to left", 256), ("per-wave powP", 512), ("16-lane powP", 3000),
+               ("8-lane powP", 9000), ("per-wave fixed-base 12-bit", 256)]
     log = []
     for ct in (False, True):
         G.ct_pow = ct
