@@ -100,7 +100,7 @@ static void words_to_elem(const Big& w, uint32_t* out) {
   for (int a = 0; a < kN; ++a) {
     const int bit = a * kLimbBits;
     uint64_t v = 0;
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 2; ++k) {  // bit % 32 + 29 <= 60: two words hold the limb (a shift by 64 would be UB)
       const int wi = bit / 32 + k;
       if (wi < (int)w.size()) v |= (uint64_t)w[wi] << (32 * k);
     }

@@ -30,7 +30,7 @@ static void words_to_elem16(const uint32_t* w, int nw, uint32_t* out) {
   for (int a = 0; a < kN; ++a) {
     const int bit = a * kLimbBits;
     uint64_t v = 0;
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 2; ++k) {  // bit % 32 + 29 <= 60: two words hold the limb (a shift by 64 would be UB)
       const int wi = bit / 32 + k;
       if (wi < nw) v |= (uint64_t)w[wi] << (32 * k);
     }
@@ -735,7 +735,7 @@ int powwave_consts_create(const uint32_t* p, const uint32_t* r2, const uint32_t*
     for (int a = 0; a < egw::kLimbs; ++a) {
       const int bit = a * egw::kBits;
       uint64_t v = 0;
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < 2; ++k) {  // bit % 32 + 29 <= 60: two words hold the limb (a shift by 64 would be UB)
         const int wi = bit / 32 + k;
         if (wi < nw) v |= (uint64_t)w[wi] << (32 * k);
       }
