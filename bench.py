@@ -269,6 +269,7 @@ def verify_tally(a, world, rank, local, dist):
     out["config"]["rccl_ranks"] = rccl_ranks
     if xch.note:
         out["config"]["exchange_note"] = xch.note
+    attach_traffic(out)
     out["modexp_per_s_per_gpu"] = {"var_base": modexp.get("var_base_per_s"),
                                    "fixed_base_g": modexp.get("fixed_base_g_per_s")} if modexp else None
     # a derived count, not a measurement: the verify step's work expressed in 256-bit
@@ -358,13 +359,17 @@ def line_common(a, world, el, value, kp, nb, man, metric, collective):
     }
     if a.pipeline == "full":
         out["config"]["pipeline"] = "full"
-    # HBM traffic of k_pow from the committed PMC passes of this same command
-    # (tools/profile_round.sh); only quoted when the profiled workload AND the library build
-    # (md5 of libeg_hip.so) match this run's.
+    return out
+
+
+def attach_traffic(out):
+    """HBM traffic of k_pow from the committed PMC passes of this same command
+    (tools/profile_round.sh); only quoted when the profiled workload (the finished config, exchange
+    fields included) AND the library build (md5 of libeg_hip.so) match this run's."""
     for prof in sorted((ROOT / "profiles").glob("r*_pmc_kpow.json"), reverse=True):  # newest round first
         try:
             pm = json.loads(prof.read_text())
-            if pm.get("bench_config") == out["config"] and pm.get("bench_build") == build_id:
+            if pm.get("bench_config") == out["config"] and pm.get("bench_build") == out.get("build"):
                 out["roofline"]["traffic"] = round(pm["traffic"]["hbm_bytes_per_launch"])
                 out["roofline"]["traffic_source"] = f"profiles/{prof.name}"
                 break
@@ -637,6 +642,7 @@ def full_pipeline(a, world, rank, local, dist, keep=None):
     out["config"]["rccl_ranks"] = rccl_ranks
     if xch.note:
         out["config"]["exchange_note"] = xch.note
+    attach_traffic(out)
     tot = nb * world * a.steps
     out["phases"] = {
         "encrypt": {"s": round(phases["encrypt"], 3), "ballots_per_s": round(tot / phases["encrypt"], 1)},
