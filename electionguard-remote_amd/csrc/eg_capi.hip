@@ -236,6 +236,9 @@ struct eg_ctx {
   // per-wave batches of at most r2l_max jobs (one per CU) run their variable parts right to left over
   // 4 waves (k_wave_job r2l; EG_WAVE_R2L=n overrides, 0 keeps the one-wave sliding window)
   size_t r2l_max = 0;
+  // per-wave batches read inputs (1) / write results (2) straight from / into the coalescer's pinned
+  // staging; default: results (2), one copy fewer per batch (EG_COALESCE_ZC=0|in|out|inout)
+  int co_zc = 2;
   bool fb_lds = false;     // A/B: eg_fb_pow_batch_dev over a 7-bit table on the LDS-staged k_fb_lds (EG_FB_LDS=1)
   int test_fail_jobs = 0;  // EG_TEST_FAIL_JOBS=k: the k-th job-table upload fails (tests of the cache's failure path)
 };
@@ -738,6 +741,10 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
         c->r2l_max = (size_t)cus;        // one 4-wave job per CU
       }
       if (const char* rl = getenv("EG_WAVE_R2L")) c->r2l_max = (size_t)std::max(0L, atol(rl));
+      if (const char* zc = getenv("EG_COALESCE_ZC")) {
+        const std::string z = zc;
+        c->co_zc = z == "in" ? 1 : z == "out" ? 2 : z == "inout" ? 3 : 0;
+      }
       c->wave_max = c->latw_jobs;
       if (const char* wm = getenv("EG_WAVE_MAX")) c->wave_max = (size_t)std::max(0L, atol(wm));
       if (const char* ws = getenv("EG_WAVE_SPLIT")) c->wave_split = ws[0] != '0';
