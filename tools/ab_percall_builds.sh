@@ -7,7 +7,7 @@
 set -eo pipefail
 TAG=${1:?tag}
 shift
-N=${N:-1100}
+N=${N:-1100}  # ballots; T: caller threads (default 11)
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$ROOT/gpurun_out"
 OUT="$ROOT/gpurun_out/${TAG}_ab_percall_builds.log"
@@ -18,7 +18,7 @@ for round in 1 2; do
     if [[ $b == new ]]; then bin="$ROOT/electionguard-remote_amd/host/_build/percall_workflow"
     elif [[ $b == env:* ]]; then bin="$ROOT/electionguard-remote_amd/host/_build/percall_workflow"; IFS=, read -ra envs <<< "${b#env:}"
     else bin="$ROOT/_ab/$b/electionguard-remote_amd/host/_build/percall_workflow"; fi
-    echo "round $round $b: $(env "${envs[@]}" timeout -k 10 300 "$bin" "$N" 11 | tail -n 1)" >> "$OUT"
+    echo "round $round $b: $(env "${envs[@]}" timeout -k 10 300 "$bin" "$N" "${T:-11}" | tail -n 1)" >> "$OUT"
     tail -n 1 "$OUT" | cut -c1-80
   done
 done
