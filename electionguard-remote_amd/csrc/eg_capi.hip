@@ -236,6 +236,10 @@ struct eg_ctx {
   // per-wave batches of at most r2l_max jobs (one per CU) run their variable parts right to left over
   // 4 waves (k_wave_job r2l; EG_WAVE_R2L=n overrides, 0 keeps the one-wave sliding window)
   size_t r2l_max = 0;
+  // per-wave batches of at most w8_max jobs without a variable exponent split their fixed-base windows
+  // over 8 waves (two per SIMD at one job per CU: n/8 + 3 multiplies of latency instead of n/4 + 2;
+  // EG_WAVE_W8=n overrides, 0 keeps 4 waves)
+  size_t w8_max = 0;
   // per-wave batches read inputs (1) / write results (2) straight from / into the coalescer's pinned
   // staging; default: results (2), one copy fewer per batch (EG_COALESCE_ZC=0|in|out|inout)
   int co_zc = 2;
@@ -739,7 +743,9 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) {
         c->latw_jobs = (size_t)cus * 4;  // one element per SIMD
         c->r2l_max = (size_t)cus;        // one 4-wave job per CU
+        c->w8_max = (size_t)cus;         // one 8-wave job per CU
       }
+      if (const char* w8 = getenv("EG_WAVE_W8")) c->w8_max = (size_t)std::max(0L, atol(w8));
       if (const char* rl = getenv("EG_WAVE_R2L")) c->r2l_max = (size_t)std::max(0L, atol(rl));
       if (const char* zc = getenv("EG_COALESCE_ZC")) {
         const std::string z = zc;

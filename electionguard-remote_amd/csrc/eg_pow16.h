@@ -62,7 +62,8 @@ struct WaveJob {
 // whose tables must then have wbits <= 8).
 // waves > 1: four waves per job, the fixed-base windows split over them (eg_pow16.hip k_wave_job); with
 // r2l the variable part runs right to left over the four waves too (the latency shape for batches of at
-// most one job per CU; with ct its constant-time schedule).
+// most one job per CU; with ct its constant-time schedule).  waves >= 8 without r2l on the
+// Montgomery-friendly p: eight waves per job (the fixed-base windows over seven or eight of them).
 int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool r2l, hipStream_t s,
                  const WaveJob* d_jobs, WaveJob dflt, uint32_t njobs, const WaveTab* d_tabs, WaveTab t_ident,
                  const uint8_t* d_bases, const uint8_t* d_exps, uint8_t* d_out, std::string* err);

@@ -206,7 +206,7 @@ __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL]
 // ahead, two register sets in turn) instead of one v_readlane per step.
 __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&pd)[kLL],
                                        const uint32_t (&pd1)[kLL], uint32_t mv) {
-  __shared__ __align__(16) uint32_t s_yb[4][kRow + 8];  // per wave of the workgroup (W <= 4)
+  __shared__ __align__(16) uint32_t s_yb[8][kRow + 8];  // per wave of the workgroup (W <= 8)
   uint32_t* yb = s_yb[threadIdx.x >> 6];
   const uint32_t ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   __builtin_amdgcn_wave_barrier();  // the previous multiply's reads of yb are done (in-order LDS)
@@ -800,10 +800,12 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool
     return 1;
   }
   const dim3 grid(njobs);
-  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1); r2l (4 waves): the
-  // variable part right to left over the 4 waves (CT: the constant-time schedule of it)
-  const int W = waves > 1 ? 4 : 1;
-  const uint32_t r2l_on = (r2l && W > 1) ? 1u : 0u;
+  // fixed-base windows split over 4 waves per job when the batch has any (waves > 1), over 8 (two per
+  // SIMD) for waves >= 8 on the Montgomery-friendly p; r2l (4 waves): the variable part right to left
+  // over the 4 waves (CT: the constant-time schedule of it)
+  const int mode = (friendly && C->d2) ? 2 : (friendly ? 1 : 0);
+  const int W = (waves >= 8 && mode == 2 && !r2l) ? 8 : waves > 1 ? 4 : 1;
+  const uint32_t r2l_on = (r2l && W == 4) ? 1u : 0u;
 #define EGW_LAUNCH(M, CTV, WV)                                                                                    \
   hipLaunchKernelGGL((egw::k_wave_job<M, CTV, WV>), grid, dim3(64 * WV), 0, s, C->d, d_jobs, dflt, njobs, d_tabs, \
                      d_bases, d_exps, d_out, t_ident, r2l_on)
@@ -814,8 +816,10 @@ int powwave_jobs(const PowWaveConsts* C, bool friendly, bool ct, int waves, bool
     else                     \
       EGW_LAUNCH(M, CTV, 1); \
   } while (0)
-  const int mode = (friendly && C->d2) ? 2 : (friendly ? 1 : 0);
-  if (ct) {
+  if (W == 8) {
+    if (ct) EGW_LAUNCH(2, true, 8);
+    else EGW_LAUNCH(2, false, 8);
+  } else if (ct) {
     if (mode == 2) EGW_LAUNCH_W(2, true);
     else if (mode == 1) EGW_LAUNCH_W(1, true);
     else EGW_LAUNCH_W(0, true);

@@ -219,3 +219,36 @@ def test_table_destroyed_with_jobs_queued(group, oracle_group):
     finally:
         group.set_coalescing(16384, 100)  # the library default
     assert got == [pow(K, e, og.p) for e in es]
+
+
+@pytest.mark.parametrize("ct", [False, True])
+@pytest.mark.parametrize("n", [1, 3, 256])
+def test_fixed_base_batches_on_eight_waves(group, oracle_group, tables, n, ct):
+    """Batches without a variable exponent, of at most one job per CU, split their fixed-base windows
+    over 8 waves (two per SIMD): one and two fixed-base terms, a product of bases times a term (wave 0
+    takes the product, seven waves the windows), edge exponents; every result equals CPython's."""
+    og = oracle_group
+    rng = random.Random(808 + n + 1000 * ct)
+    g_t, k_t, k8 = tables["g"][0], tables["K12"][0], tables["K8"][0]
+    K, K2 = tables["K12"][1], tables["K8"][1]
+    edges = _edges(og)
+    group.ct_pow = ct
+    try:
+        subs = []
+        for i in range(n):
+            a = edges[i % len(edges)] if i < 2 * len(edges) else rng.randrange(og.q)
+            b = rng.randrange(og.q)
+            kind = i % 4
+            if kind == 0:
+                subs.append((group.mexp_submit([], None, [(k8, a)]), pow(K2, a, og.p)))
+            elif kind == 1:
+                subs.append((group.mexp_submit([], None, [(g_t, a), (k8, b)]), pow(og.g, a, og.p) * pow(K2, b, og.p) % og.p))
+            elif kind == 2:  # constant time: the 12-bit table takes its 6-bit companion
+                subs.append((group.mexp_submit([], None, [(k_t, a), (g_t, b)]), pow(K, a, og.p) * pow(og.g, b, og.p) % og.p))
+            else:
+                al = rng.randrange(og.p)
+                subs.append((group.mexp_submit([al], None, [(g_t, a)]), al * pow(og.g, a, og.p) % og.p))
+        bad = [i for i, (t, want) in enumerate(subs) if int.from_bytes(t.wait(), "big") != want]
+    finally:
+        group.ct_pow = False
+    assert not bad, bad[:8]
