@@ -4,7 +4,11 @@ Reference: ``service DecryptingTrusteeService`` (src/main/proto/decrypting_trust
 over the messages of src/main/proto/common.proto:8-28 and common_rpc.proto:8-14 (no
 ``package`` statement, so the method paths are ``/DecryptingTrusteeService/<method>``).
 ``protoc`` / ``grpc_tools`` are not in the image, so the descriptors are built here
-programmatically with the reference's message names and field numbers.
+programmatically with the reference's message names and field numbers.  They are pinned to the
+reference's own IDL: tools/extract_proto_fields.py parses its .proto files into
+tests/golden/reference_proto_fields.json, and tests/test_remote_wire.py requires POOL to equal
+that table in both directions (every field's name, number, type, label and type name, reserved
+ranges, the service's methods).
 
 * :class:`DecryptingTrusteeServer` — the trustee process (``RunRemoteDecryptingTrustee``,
   RunRemoteDecryptingTrustee.java:58-120, handlers :180-247): each RPC is ONE GPU batch;

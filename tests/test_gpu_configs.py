@@ -1,15 +1,14 @@
 """GPU: the BASELINE.json configurations at one GPU's full share, checked through
 size-independent properties (the CPU oracle cannot redo them in a test's time):
 
-* configs[2] -- 8 x MI355X verify + tally of 1M ballots sharded by ballot: ONE rank's shard of
-  125,000 ballots (4 x 5 manifest), device-resident as bench.py runs it.  Every verdict is
-  valid; the tally decrypts (joint secret, BSGS dLog) to exactly the per-selection vote sums;
-  and the two-rank fold (each half verified alone, partial tallies multiplied mod p as
+* configs[4]'s manifest (20 x 5): 10,000 ballots, device-resident as bench.py runs them.  Every
+  verdict is valid; the tally decrypts (joint secret, BSGS dLog) to exactly the per-selection
+  vote sums; and the two-rank fold (each half verified alone, partial tallies multiplied mod p as
   electionguard.distributed.gather_fold_tally does on rank 0) equals the single tally.
-* configs[4] -- the 100-selection manifest (20 x 5): 10,000 ballots, same checks; and one GPU's
-  full share of configs[4] on 8 GPUs, 125,000 ballots, whose tally is decrypted through the
-  DecryptingTrustee shares (5 guardians, quorum 3, 2 missing: direct + compensated shares with
-  proofs checked, Lagrange combine, BSGS dLog) to the exact vote sums.
+
+configs[2] and configs[4] at their full 1M ballots (8 shards of 125,000, the 8-part fold,
+threshold decryption through DecryptingTrustees) are tests/test_gpu_config_1M.py; they subsume the
+one-rank 125k-shard tests this file held until round 5.
 """
 import numpy as np
 import pytest
@@ -86,18 +85,5 @@ def _run(group, contests, selections, nb, seed, trustees=False):
     assert np.array_equal(group.tally_allgather_fold(d2, 2, man.n_real * 2).reshape(man.n_real, 2, 512), T)
 
 
-def test_config2_one_rank_shard_125k(group):
-    _run(group, 4, 5, 125_000, 21)
-
-
 def test_config4_shape_100_selections(group):
     _run(group, 20, 5, 10_000, 23)
-
-
-@pytest.mark.timeout(600)
-def test_config4_one_rank_shard_125k_trustee_decryption(group):
-    """configs[4] (1M ballots x 100 selections over 8 GPUs): one GPU's 125,000-ballot share."""
-    import time
-    t = time.time()
-    _run(group, 20, 5, 125_000, 27, trustees=True)
-    print(f"configs[4] one-rank shard: 125,000 ballots x 120 selections, {time.time() - t:.1f} s")

@@ -2,7 +2,11 @@
 oracle-backed stand-in trustee — message layout, field numbers, error-string convention
 (RunRemoteDecryptingTrustee.java:200-204) and the proxy's empty-list-on-error contract
 (RemoteDecryptingTrusteeProxy.java:64-66)."""
+import copy
+import json
 import random
+import sys
+from pathlib import Path
 
 import pytest
 
@@ -42,16 +46,121 @@ def setup():
     return G, gs, K, qbar, texts
 
 
-def test_descriptors_match_reference_field_numbers():
+REF_FIELDS = Path(__file__).resolve().parent / "golden" / "reference_proto_fields.json"
+
+
+def _pool_files(pool):
+    """The FileDescriptorProtos behind electionguard.remote.POOL (what the server and proxy speak)."""
+    from google.protobuf import descriptor_pb2
+    out = {}
+    for name in ("common.proto", "common_rpc.proto", "decrypting_trustee_rpc.proto"):
+        fdp = descriptor_pb2.FileDescriptorProto()
+        pool.FindFileByName(name).CopyToProto(fdp)
+        out[name] = fdp
+    return out
+
+
+def wire_mismatches(files, ref) -> list:
+    """Compare FileDescriptorProtos with the reference's extracted .proto table (both directions):
+    every message and service the files define must exist in the reference's same-named file with
+    the same fields (name, number, type, label, type name) and reserved ranges, and every message
+    the reference's DecryptingTrusteeService reaches (requests, responses and the messages their
+    fields name, transitively) must be defined here.  -> list of differences (empty = identical)."""
+    from google.protobuf import descriptor_pb2
+    F = descriptor_pb2.FieldDescriptorProto
+    bad, have = [], {}
+    for fn, fdp in files.items():
+        rfile = ref["files"].get(fn)
+        if rfile is None:
+            bad.append(f"{fn}: no such reference file")
+            continue
+        if list(fdp.dependency) != rfile["imports"]:
+            bad.append(f"{fn}: imports {list(fdp.dependency)} != {rfile['imports']}")
+        if (fdp.package or None) != rfile["package"]:
+            bad.append(f"{fn}: package {fdp.package!r} != {rfile['package']!r}")
+        for m in fdp.message_type:
+            have["." + m.name] = m
+            rm = rfile["messages"].get(m.name)
+            if rm is None:
+                bad.append(f"{fn}: message {m.name} not in the reference")
+                continue
+            mine = sorted((f.name, f.number, F.Type.Name(f.type), F.Label.Name(f.label), f.type_name or None)
+                          for f in m.field)
+            theirs = sorted((f["name"], f["number"], f["type"], f["label"], f["type_name"]) for f in rm["fields"])
+            if mine != theirs:
+                bad.append(f"{fn}: {m.name} fields {mine} != reference {theirs}")
+            rr = sorted([r.start, r.end] for r in m.reserved_range) + sorted(m.reserved_name)
+            if rr != sorted(x for x in rm["reserved"] if isinstance(x, list)) + sorted(
+                    x for x in rm["reserved"] if isinstance(x, str)):
+                bad.append(f"{fn}: {m.name} reserved {rr} != reference {rm['reserved']}")
+        for s in fdp.service:
+            rs = rfile["services"].get(s.name)
+            mine = [(x.name, x.input_type, x.output_type) for x in s.method]
+            theirs = None if rs is None else [(x["name"], x["input"], x["output"]) for x in rs]
+            if mine != theirs:
+                bad.append(f"{fn}: service {s.name} methods {mine} != reference {theirs}")
+    # reference -> here: everything the trustee service reaches
+    rmsgs = {"." + n: m for f in ref["files"].values() for n, m in f["messages"].items()}
+    todo = [t for x in ref["files"]["decrypting_trustee_rpc.proto"]["services"]["DecryptingTrusteeService"]
+            for t in (x["input"], x["output"])]
+    seen = set()
+    while todo:
+        t = todo.pop()
+        if t in seen:
+            continue
+        seen.add(t)
+        if t not in have:
+            bad.append(f"reference message {t} (reached from DecryptingTrusteeService) is not defined here")
+        todo.extend(f["type_name"] for f in rmsgs[t]["fields"] if f["type_name"])
+    return bad
+
+
+def test_wire_descriptors_match_the_reference_protos():
+    """electionguard.remote.POOL == the reference's own .proto files (decrypting_trustee_rpc.proto:9-45,
+    common.proto:8-28, common_rpc.proto:6-12), via the table tools/extract_proto_fields.py extracted."""
     from electionguard.remote import POOL
-    f = POOL.FindMessageTypeByName("GenericChaumPedersenProof").fields_by_name
-    assert (f["challenge"].number, f["response"].number) == (3, 4)
-    c = POOL.FindMessageTypeByName("CompensatedDecryptionRequest").fields_by_name
-    assert (c["extended_base_hash"].number, c["missing_guardian_id"].number, c["text"].number) == (1, 2, 3)
-    r = POOL.FindMessageTypeByName("CompensatedDecryptionResult").fields_by_name
-    assert r["recoveryPublicKey"].number == 3
-    svc = POOL.FindServiceByName("DecryptingTrusteeService")
-    assert [m.name for m in svc.methods] == ["directDecrypt", "compensatedDecrypt", "finish"]
+    ref = json.loads(REF_FIELDS.read_text())
+    assert wire_mismatches(_pool_files(POOL), ref) == []
+
+
+def test_wire_check_catches_one_field_edits():
+    """A one-field edit of either side -- the reference table or the hand-built descriptors -- fails."""
+    from electionguard.remote import POOL
+    ref = json.loads(REF_FIELDS.read_text())
+    # reference side: renumber, rename, retype, relabel one field; drop a reserved range; rename a method
+    edits = [("challenge", "number", 5), ("challenge", "name", "c"), ("response", "type_name", ".ElementModP"),
+             ("response", "label", "LABEL_REPEATED")]
+    for fname, key, val in edits:
+        r = copy.deepcopy(ref)
+        f = next(x for x in r["files"]["common.proto"]["messages"]["GenericChaumPedersenProof"]["fields"]
+                 if x["name"] == fname)
+        f[key] = val
+        assert wire_mismatches(_pool_files(POOL), r), (fname, key, val)
+    r = copy.deepcopy(ref)
+    r["files"]["common.proto"]["messages"]["GenericChaumPedersenProof"]["reserved"].pop()
+    assert wire_mismatches(_pool_files(POOL), r)
+    r = copy.deepcopy(ref)
+    r["files"]["decrypting_trustee_rpc.proto"]["services"]["DecryptingTrusteeService"][2]["output"] = ".FinishRequest"
+    assert wire_mismatches(_pool_files(POOL), r)
+    # our side: one field of one request, a missing message, one method
+    files = _pool_files(POOL)
+    next(f for m in files["decrypting_trustee_rpc.proto"].message_type if m.name == "CompensatedDecryptionRequest"
+         for f in m.field if f.name == "text").number = 4
+    assert wire_mismatches(files, ref)
+    files = _pool_files(POOL)
+    del files["common.proto"].message_type[[m.name for m in files["common.proto"].message_type].index("ElementModQ")]
+    assert wire_mismatches(files, ref)
+    files = _pool_files(POOL)
+    files["decrypting_trustee_rpc.proto"].service[0].method[0].input_type = ".CompensatedDecryptionRequest"
+    assert wire_mismatches(files, ref)
+
+
+@pytest.mark.skipif(not Path("/root/reference/src/main/proto").is_dir(), reason="the reference is not on this host")
+def test_committed_table_is_the_reference_extraction():
+    """Where the reference is present, re-extracting its .proto files gives the committed table."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
+    import extract_proto_fields
+    assert extract_proto_fields.extract() == json.loads(REF_FIELDS.read_text())
 
 
 def test_direct_and_compensated_over_grpc(setup):
