@@ -64,7 +64,10 @@ def parse(argv=None):
     ap.add_argument("--quorum", type=int, default=3)
     ap.add_argument("--available", type=int, default=3, help="--pipeline full: guardians present at decryption")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
-                    help="seconds a collective (and the rank launcher) may wait before failing")
+                    help="seconds a host (gloo) collective may wait before failing")
+    ap.add_argument("--strict-rccl", type=int, choices=(0, 1), default=None,
+                    help="1 = a rank that cannot open its RCCL communicator fails the run (non-zero exit) "
+                         "instead of falling back to a host exchange; default 1 at --gpus N > 1 in RCCL mode")
     ap.add_argument("--fb-window", type=int, default=22, help="fixed-base radix window bits for g and K")
     ap.add_argument("--cpu-sample", type=int, default=1, help="run the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline sample")
@@ -82,7 +85,35 @@ def parse(argv=None):
         a.contests = 20 if a.manifest == "large" else 4
     if not a.ballots:
         a.ballots = default_ballots(a.gpus, a.pipeline)
+    if a.strict_rccl is None:
+        a.strict_rccl = 1 if a.gpus > 1 and exchange_mode() == "rccl" else 0
     return a
+
+
+COMM_TIMEOUT_S = 120.0  # EG_COMM_TIMEOUT_S the ranks get unless the caller set one
+
+
+def comm_timeout_s() -> float:
+    """The deadline libeg gives every RCCL init and collective (eg_capi_comm.inc comm_wait_locked)."""
+    try:
+        v = float(os.environ.get("EG_COMM_TIMEOUT_S", COMM_TIMEOUT_S))
+    except ValueError:
+        v = COMM_TIMEOUT_S
+    return v if v > 0 else COMM_TIMEOUT_S
+
+
+def launch_budget_s(a) -> float:
+    """How long the self-launcher lets N ranks run before it kills them (returns 124): the work the
+    run is sized for, with room, plus one communicator deadline -- a rank stuck in a collective
+    fails on its own after comm_timeout_s() (and the launcher then ends the others at once), so
+    this is only the backstop for a rank stuck anywhere else.  Per-step allowance: 30 us per
+    4 x (5+1) ballot on one MI355X (3.8 s per 125k-ballot step) scaled by selections, times 4;
+    the full pipeline adds its encryption and decryption; setup covers the first `import torch`
+    on a fresh box, the 22-bit tables, the ballots' encryption and the CPU baseline."""
+    nsel = a.contests * (a.selections + 1)
+    per_step = 4 * 30e-6 * a.ballots * nsel / 24 * (1.5 if a.pipeline == "full" else 1.0)
+    setup = 300.0 + 4 * a.cpu_seconds + (60.0 if a.modexp_n else 0.0) + 4 * 30e-6 * a.ballots * nsel / 24
+    return setup + (a.steps + a.warmup) * per_step + comm_timeout_s()
 
 
 def default_ballots(gpus: int, pipeline: str = "verify") -> int:
@@ -159,7 +190,11 @@ def main(argv=None):
         # no launcher: start one rank process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*) before
         # anything touches HIP; rank 0 prints the JSON line; the first rank to fail ends the run
         # (the others are killed) and its status is this process's
-        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus, timeout=a.dist_timeout * 4))
+        env = dict(os.environ)
+        env.setdefault("EG_COMM_TIMEOUT_S", str(COMM_TIMEOUT_S))
+        sys.exit(run_ranks(str(Path(__file__).resolve()), sys.argv[1:], a.gpus, timeout=launch_budget_s(a), env=env))
+    if a.gpus > 1:
+        os.environ.setdefault("EG_COMM_TIMEOUT_S", str(COMM_TIMEOUT_S))  # ranks started by torch.distributed.run
     world, rank, local, dist = init_ranks(a)
     if a.pipeline == "full":
         out = full_pipeline(a, world, rank, local, dist)
@@ -230,7 +265,7 @@ def verify_tally(a, world, rank, local, dist):
     # modexp/sec/GPU microbenchmark on rank 0, before the verify step so the verify
     # launches stay the last k_pow dispatches of the process (tools/prof_summary.py)
     modexp = modexp_ubench(group, a.modexp_n, rank) if a.modexp_n > 0 and rank == 0 else None
-    xch = TallyExchange(group, dist, world, rank, exchange_mode())
+    xch = TallyExchange(group, dist, world, rank, exchange_mode(), fallback=not a.strict_rccl)
     ver = Verifier(group, key, qbar, man)
     final_tally = None
 
@@ -582,7 +617,7 @@ def full_pipeline(a, world, rank, local, dist, keep=None):
         comm = {g.gid: g.commitments for g in gk}
         dec = Decryption(group, qbar, [DecryptingTrustee(group, g, comm) for g in gk[:a.available]],
                          [g.gid for g in gk[a.available:]], {g.gid: g.public_key for g in gk})
-    xch = TallyExchange(group, dist, world, rank, exchange_mode())
+    xch = TallyExchange(group, dist, world, rank, exchange_mode(), fallback=not a.strict_rccl)
     ph = {"encrypt": 0.0, "verify_tally": 0.0, "exchange": 0.0, "decrypt": 0.0}
     counts = None
     last = {}

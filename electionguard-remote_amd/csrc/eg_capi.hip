@@ -199,6 +199,7 @@ struct eg_ctx {
   uint32_t use_comb = 1;                // two-exponent jobs use the Lim-Lee comb (EG_NO_COMB=1 to disable)
   uint32_t ct_encrypt = 0;              // encryption on k_pow<F, true> with small CT tables (eg_ctx_set_ct_encrypt)
   uint32_t ct_pow = 0;                  // powP / fixed-base / per-element calls constant-time (eg_ctx_set_ct_pow)
+  std::atomic<uint32_t> ct_pow_submit{0};  // the same switch as per-element submits read it (no ctx lock)
   int ct_window = kCtEncWindow;         // their radix width
   eg_fixed_base* g_ct = nullptr;  // g's kCtEncWindow-bit table (K's live in keys[].ct)
   uint32_t ct_rows = 4;                 // trustee pair comb rows (EG_CT_ROWS=5: one 32-entry block)
@@ -221,6 +222,11 @@ struct eg_ctx {
   hipEvent_t up_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
   void* comm = nullptr;  // RCCL communicator of the multi-GPU exchange (eg_comm_init; eg_capi_comm.inc)
   int comm_world = 1, comm_rank = 0;
+  // sticky after a communicator was aborted (a collective that timed out or failed, an init that did):
+  // every collective and the fold fail with EG_ERR_STATE until eg_comm_destroy / eg_comm_init, so a
+  // retry can never fold the local parts alone and call that the tally
+  bool comm_failed = false;
+  std::string comm_fail_msg;
   // the latency-shaped powP layouts (eg_pow16.hip) for the coalescer's small batches: one element
   // per wave for batches up to one per SIMD (latw_jobs), 16-lane groups up to one resident round
   // (lat_jobs); EG_LATENCY_POW=0 keeps every batch on the 8-lane layout, =16 skips the per-wave one

@@ -138,13 +138,18 @@ class TallyExchange:
             # world keeps the exchange on the host (the line says so, rccl_ranks = 0) instead of dying
             if not ready:
                 if fallback:
-                    if err is None and group.comm_info()[0]:
+                    # every rank drops what it has: a live communicator, or (the rank whose init
+                    # failed) the context's sticky aborted-communicator state
+                    try:
                         group.comm_destroy()
+                    except Exception as e:  # noqa: BLE001 - the host exchange does not need it
+                        import sys
+                        print(f"rank {rank}: comm_destroy after a failed init: {e}", file=sys.stderr, flush=True)
                     self.mode = "gloo"
                     self.note = f"RCCL communicator unavailable ({err or 'on another rank'}): host exchange"
                     import sys
                     print(f"rank {rank}: {self.note}", file=sys.stderr, flush=True)
-                else:
+                else:  # strict (bench.py --strict-rccl, the default at N > 1): every rank fails
                     raise RuntimeError(f"eg_comm_init failed: {err or 'on another rank'}")
 
     @property

@@ -40,8 +40,9 @@ import java.math.BigInteger
  * GPU round trip per point where upstream's code looks at a value.  Results are the same integers.
  * `multInv` / `div` of a value that is not a fixed-base expression stay on the upstream element (host
  * BigInteger), as does everything off the hot path.  Measured through the same API in C++
- * (tests/cpp/percall_workflow.cpp, profiles/r05*_percall_workflow.json): encrypt 2.7x, verify 1.85x,
- * the one-thread tally 5.4x the CPU port on 11 threads.
+ * (tests/cpp/percall_workflow.cpp, final library profiles/r05zs_percall_workflow.json): encrypt 2.2x,
+ * verify 2.3x, the one-thread tally 6.9x the CPU port on 11 threads; the caller's thread count
+ * (nthreads = 11 at RunRemoteWorkflowTest.java:140,180) against the batch rate: INTEGRATION.md §1.
  *
  * A trustee's context ([trustee]) runs every exponentiation on the constant-time schedules
  * (`eg_ctx_set_ct_pow`): its secret shares s_i, P_l(x_i) reach `powP` through this adapter

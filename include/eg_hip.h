@@ -235,11 +235,17 @@ int eg_verify_shares(eg_ctx* ctx, const uint8_t qbar_be[EG_Q_BYTES], const uint8
  * the ticket is waited).  eg_*_submit queues one job on the ctx's open batch and returns a ticket at
  * once; a dispatcher thread runs the batch as ONE launch of the per-wave job kernel (every mix of
  * kinds side by side; large batches of one plain kind on the throughput layouts) once the GPU is
- * free and the oldest job has waited window_us, or when max_batch jobs are queued.  The caller's out
+ * free and the oldest job has waited its window, or as many jobs are queued as the previous batch
+ * took, or max_batch jobs are queued.  The window is ADAPTIVE by default (half as long as the
+ * previous batch ran, within [20 us, 100 us]); eg_ctx_set_coalescing(ctx, max_batch, window_us)
+ * with window_us > 0 fixes it at exactly window_us, window_us = 0 restores the adaptive default
+ * (EG_COALESCE_WINDOW_US=n in the environment also fixes it).  A job records eg_ctx_set_ct_pow's
+ * setting when it is SUBMITTED and runs in that mode; a batch never mixes modes (a job of the other
+ * mode closes the open batch, which is dispatched first).  The caller's out
  * must stay valid until eg_ticket_wait, which blocks until the result is in out, frees the ticket
  * and returns the batch's status.  eg_ctx_destroy first runs every queued job, and a ticket stays
  * waitable after it (each ticket must still be waited once, to free it); submits racing destroy fail
- * with EG_ERR_STATE.  eg_*_one = submit + wait.  Defaults: max_batch 16384, window 100 us.
+ * with EG_ERR_STATE.  eg_*_one = submit + wait.  Defaults: max_batch 16384, adaptive window.
  *   eg_powp_submit   : base^exp                    (ElementModP.powP)
  *   eg_gpowp_submit  : g^exp, g's table            (GroupContext.gPowP)
  *   eg_fb_pow_submit : base^exp over fb's table    (an accelerated element's powP: acceleratePow(),

@@ -137,7 +137,7 @@ int main(int argc, char** argv) {
     sweep += buf;
     if (m == n) break;
   }
-  check(eg_ctx_set_coalescing(ctx, 16384, 100), "eg_ctx_set_coalescing");
+  check(eg_ctx_set_coalescing(ctx, 16384, 0), "eg_ctx_set_coalescing");  // the adaptive default
   printf("{\"n\": %u, \"threads\": %d, \"mismatches\": %ld, \"sweep\": [%s], \"powp_batch_per_s\": %.1f, "
          "\"powp_one_blocking_per_s\": %.1f, \"multp_one_blocking_per_s\": %.1f, \"gpowp_one_blocking_per_s\": %.1f, "
          "\"powp_submit_wait_per_s\": %.1f}\n",

@@ -260,7 +260,81 @@ def test_rccl_init_failure_falls_back_to_the_host_exchange():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got == [(0, "gloo", "gloo (host)", True, True), (1, "gloo", "gloo (host)", False, True)]
+    # both ranks drop their communicator state: rank 0 its live one, rank 1 its failed init's
+    assert got == [(0, "gloo", "gloo (host)", True, True), (1, "gloo", "gloo (host)", True, True)]
+
+
+def _strict_worker(rank, world, port, q):
+    """TallyExchange(fallback=False) -- bench.py --strict-rccl, its default at N > 1 -- where rank 1
+    cannot create its communicator: EVERY rank raises (the run exits non-zero instead of printing a
+    scaling number for a host exchange)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from electionguard.distributed import TallyExchange
+
+    class FakeGroup:
+        comm = None
+
+        @staticmethod
+        def comm_unique_id():
+            return bytes(range(128))
+
+        def comm_init(self, uid, w, r):
+            if rank == 1:
+                raise RuntimeError("no RCCL here")
+            self.comm = (w, r)
+
+        def comm_info(self):
+            return self.comm or (0, 0)
+
+        def comm_destroy(self):
+            self.comm = None
+
+    try:
+        TallyExchange(FakeGroup(), dist, world, rank, "rccl", fallback=False)
+        q.put((rank, "no error"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_strict_rccl_fails_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strict_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got[0] == (0, "eg_comm_init failed: on another rank")
+    assert got[1][0] == 1 and "no RCCL here" in got[1][1]
+
+
+def test_bench_strict_rccl_default_and_launch_budget(monkeypatch):
+    """bench.py: --strict-rccl is on by default at N > 1 in RCCL mode (off for the gloo rehearsal and
+    at N = 1); the self-launcher's kill deadline is the run's own budget plus ONE communicator
+    deadline (EG_COMM_TIMEOUT_S), not 4 x --dist-timeout (VERDICT r05 weak #5)."""
+    import importlib
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    bench = importlib.import_module("bench")
+    monkeypatch.delenv("EG_DIST_BACKEND", raising=False)
+    monkeypatch.delenv("EG_COMM_TIMEOUT_S", raising=False)
+    assert bench.parse(["--gpus", "8"]).strict_rccl == 1
+    assert bench.parse(["--gpus", "1"]).strict_rccl == 0
+    assert bench.parse(["--gpus", "8", "--strict-rccl", "0"]).strict_rccl == 0
+    monkeypatch.setenv("EG_DIST_BACKEND", "gloo")
+    assert bench.parse(["--gpus", "8"]).strict_rccl == 0
+    monkeypatch.delenv("EG_DIST_BACKEND")
+    a = bench.parse(["--gpus", "8", "--steps", "20", "--warmup", "5"])
+    budget = bench.launch_budget_s(a)
+    assert bench.comm_timeout_s() == bench.COMM_TIMEOUT_S
+    assert 600 < budget < 1200 < 4 * a.dist_timeout, budget
+    monkeypatch.setenv("EG_COMM_TIMEOUT_S", "30")
+    assert bench.launch_budget_s(a) == pytest.approx(budget - bench.COMM_TIMEOUT_S + 30)
 
 
 def test_world8_exchange_rccl_ranks_and_fallback(tmp_path):

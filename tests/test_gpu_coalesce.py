@@ -114,9 +114,40 @@ def test_coalescing_window_and_errors(group):
     group.set_coalescing(4, 50)
     out = group.powP_one(3, 5)
     assert int.from_bytes(out, "big") == 243
-    group.set_coalescing(16384, 100)
+    group.set_coalescing(16384, 0)  # the adaptive default
     with pytest.raises(native.EgError):
         group.set_coalescing(0, 100)
+
+
+def test_constant_time_mode_recorded_per_job(group, oracle_group):
+    """eg_ctx_set_ct_pow is read when a job is SUBMITTED: jobs queued with the switch on stay in a
+    constant-time batch even when the switch goes off before their batch runs, and the jobs submitted
+    after it form a separate batch (a batch never mixes modes).  A fixed 30 ms window
+    keeps the first jobs queued while the switch changes; every result equals CPython's."""
+    import random
+    og = oracle_group
+    rng = random.Random(5150)
+    subs = []
+    group.set_coalescing(16384, 30000)
+    try:
+        group.multP_one(1, 1)  # the previous dispatch took one job
+        group.ct_pow = True
+        for i in range(6):  # secret-exponent jobs: g^x and b^x
+            x = rng.randrange(og.q)
+            b = rng.randrange(og.p)
+            subs.append((group.mexp_submit([], None, [(None, x)]), pow(og.g, x, og.p)))
+            subs.append((group.mexp_submit([b], x), pow(b, x, og.p)))
+        group.ct_pow = False  # returns at once: no batch is running, the queued ones keep their mode
+        for i in range(6):
+            x = rng.randrange(og.q)
+            subs.append((group.mexp_submit([], None, [(None, x)]), pow(og.g, x, og.p)))
+        group.ct_pow = True
+        subs.append((group.mexp_submit([7], 11), pow(7, 11, og.p)))
+        got = [int.from_bytes(t.wait(), "big") for t, _ in subs]
+    finally:
+        group.ct_pow = False
+        group.set_coalescing(16384, 0)
+    assert got == [w for _, w in subs]
 
 
 def test_ticket_outlives_context(group):

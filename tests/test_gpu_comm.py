@@ -1,7 +1,8 @@
 """libeg_hip's own device memory, verdict reduction and multi-GPU tally exchange,
 on one MI355X: eg_dev_alloc / eg_memcpy_* / eg_all_nonzero_dev, the RCCL communicator at world
 size 1 (eg_comm_init / eg_comm_all_valid) and eg_tally_allgather_fold bit-exact against the
-oracle's fold; the job-table cache's failure path and two election keys alternating
+oracle's fold, every collective's completion polled under the deadline (a stalled one aborted, the
+failure sticky); the job-table cache's failure path and two election keys alternating
 on one context."""
 import random
 
@@ -83,6 +84,53 @@ def test_rccl_world_one_exchange(group, oracle_group):
     one = _rand_elems(rng, 6, p).reshape(3, 2, 512)
     assert np.array_equal(x.fold(group.to_device(one), 3), one)  # world 1: the local tally itself
     assert x.all_valid(True) and not x.all_valid(False)
+
+
+@pytest.mark.parametrize("where", ["all_valid", "fold"])
+def test_rccl_collective_deadline_and_sticky_failure(group, oracle_group, monkeypatch, where):
+    """A collective whose completion never arrives (EG_TEST_COMM_STALL=1: libeg's wait never sees the
+    event, as with a peer that died after the enqueue) fails within the deadline (EG_COMM_TIMEOUT_S)
+    instead of hanging in hipStreamSynchronize; the communicator is aborted and the failure is
+    STICKY: every later collective AND the fold fail with EG_ERR_STATE (no silent local-parts fold
+    that would be a partial tally), until eg_comm_destroy resets the context."""
+    import time
+
+    from electionguard.core.native import EgError
+    rng = random.Random(41)
+    p = oracle_group.p
+    n = 8
+    parts = _rand_elems(rng, n, p).reshape(1, n, 512)
+    d = group.to_device(parts)
+    monkeypatch.setenv("EG_COMM_TIMEOUT_S", "1.5")
+    group.comm_init(group.comm_unique_id(), 1, 0)
+    try:
+        monkeypatch.setenv("EG_TEST_COMM_STALL", "1")
+        t = time.monotonic()
+        with pytest.raises(EgError) as e:
+            if where == "all_valid":
+                group.comm_all_valid(True)
+            else:
+                group.tally_allgather_fold(d, 1, n)
+        took = time.monotonic() - t
+        assert e.value.code == 2 and "not complete after" in str(e.value), str(e.value)
+        assert 1.4 <= took < 10, took
+        monkeypatch.delenv("EG_TEST_COMM_STALL")
+        assert group.comm_info() == (0, 0)  # aborted
+        for call in (lambda: group.comm_all_valid(True), lambda: group.tally_allgather_fold(d, 1, n)):
+            with pytest.raises(EgError) as e:
+                call()
+            assert e.value.code == 5 and "aborted" in str(e.value), str(e.value)
+    finally:
+        monkeypatch.delenv("EG_TEST_COMM_STALL", raising=False)
+        group.comm_destroy()  # resets the sticky failure
+    out = group.tally_allgather_fold(d, 1, n)  # a clean context folds its local parts again
+    assert np.array_equal(out, parts[0])
+    group.comm_init(group.comm_unique_id(), 1, 0)  # and a new communicator works through the polled wait
+    try:
+        assert group.comm_all_valid(True) is True
+        assert np.array_equal(group.tally_allgather_fold(d, 1, n), parts[0])
+    finally:
+        group.comm_destroy()
 
 
 def test_job_cache_survives_a_failed_upload(oracle_group):

@@ -211,14 +211,19 @@ def test_table_destroyed_with_jobs_queued(group, oracle_group):
     K = pow(og.g, rng.randrange(og.q), og.p)
     fb = group.fixed_base(K, 8)
     es = [rng.randrange(og.q) for _ in range(40)]
-    group.set_coalescing(4096, 20000)  # a 20 ms window: the jobs are still queued at the close
+    import time
+    group.set_coalescing(4096, 20000)  # a FIXED 20 ms window (honoured exactly): still queued at the close
     try:
+        group.multP_one(1, 1)  # the previous dispatch took 1 job: 40 jobs do not end the window early
+        t = time.monotonic()
         ts = [group.mexp_submit([], None, [(fb, e)]) for e in es]
         fb.close()
+        waited = time.monotonic() - t
         got = [int.from_bytes(t.wait(), "big") for t in ts]
     finally:
-        group.set_coalescing(16384, 100)  # the library default
+        group.set_coalescing(16384, 0)  # the library default (adaptive window)
     assert got == [pow(K, e, og.p) for e in es]
+    assert waited >= 0.015, f"close returned after {waited * 1e3:.1f} ms: the jobs were not queued"
 
 
 @pytest.mark.parametrize("ct", [False, True])
