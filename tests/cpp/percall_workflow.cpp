@@ -249,11 +249,14 @@ int main(int argc, char** argv) {
     encryptBallot(E, 0, c1.data(), r1.data(), p1.data());
     verifyBallot(E, 0, cts_ref.data(), rp_ref.data(), cp_ref.data(), o1.data(), o2.data());
   }
+  G.setCoalescing(16384, 0);  // the library defaults (with EG_COALESCE_STATS=1: the warm-up's batch statistics)
   const double gpu_enc_s = run_threads(guarded([&](size_t b) { encryptBallot(E, b, cts.data(), rp.data(), cp.data()); }));
+  G.setCoalescing(16384, 0);  // (EG_COALESCE_STATS=1: the encryption phase's statistics)
   const long enc_mis = (long)(cts != cts_ref) + (long)(rp != rp_ref) + (long)(cp != cp_ref);
   std::vector<uint8_t> oks(nb * kNSEL), okc(nb * kNC);
   const double gpu_ver_s =
       run_threads(guarded([&](size_t b) { verifyBallot(E, b, cts_ref.data(), rp_ref.data(), cp_ref.data(), oks.data(), okc.data()); }));
+  G.setCoalescing(16384, 0);  // (EG_COALESCE_STATS=1: the verification phase's statistics)
   long ver_mis = 0, invalid = 0;
   for (size_t i = 0; i < oks.size(); ++i) ver_mis += oks[i] != oks_ref[i], invalid += !oks[i];
   for (size_t i = 0; i < okc.size(); ++i) ver_mis += okc[i] != okc_ref[i], invalid += !okc[i];
