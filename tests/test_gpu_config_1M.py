@@ -43,7 +43,7 @@ def _shard_inputs(seed, k, man, q):
     return votes, random_scalars(rng, (SHARD, man.nsel, 4), q), random_scalars(rng, (SHARD, man.n_contests), q)
 
 
-def _full_pipeline_1M(group, contests, seed, nspoiled):
+def _full_pipeline_1M(group, contests, seed, nspoiled, say=print):
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption_device
     from electionguard.decrypt import Decryption, DecryptingTrustee, verify_decryption_record
     from electionguard.keyceremony import key_ceremony, verify_backups, verify_commitment_proofs
@@ -103,6 +103,7 @@ def _full_pipeline_1M(group, contests, seed, nspoiled):
             if k == 0 and nspoiled:
                 spoiled_cts = cts[0:nspoiled].download()
                 spoiled_votes = real[:nspoiled]
+            say(f"  shard {k + 1}/{SHARDS}: {(k + 1) * SHARD} ballots, encrypt {t_enc:.1f} s, verify+tally {t_ver:.1f} s")
     del cts, rp, cp, dsn, dcn, dv, oks, okc
     # rank 0's fold after the all-gather: parts laid out (world, n_real * 2, 512) as ncclAllGather leaves them
     gathered = np.ascontiguousarray(np.stack(parts)).reshape(SHARDS, man.n_real * 2, 512)
@@ -129,19 +130,28 @@ def _full_pipeline_1M(group, contests, seed, nspoiled):
                                        max_count=man.votes_allowed)
         assert all(rvs.values()), rvs
     n = SHARDS * SHARD
-    print(f"\n{contests}x(5+1), {n} ballots ({nspoiled} spoiled) on one GPU: encrypt {t_enc:.1f} s "
+    say(f"{contests}x(5+1), {n} ballots ({nspoiled} spoiled) on one GPU: encrypt {t_enc:.1f} s "
           f"({n / t_enc:.0f}/s), verify+tally {t_ver:.1f} s ({n / t_ver:.0f}/s), threshold decryption "
           f"{t_dec:.2f} s, all {time.time() - t_all:.1f} s; counts exact, record checks {rv}")
 
 
+def _say(capsys):
+    """Progress straight to the terminal, past pytest's capture: a 3-minute test must not look hung
+    to a runner that watches the output."""
+    def say(msg):
+        with capsys.disabled():
+            print(msg, flush=True)
+    return say
+
+
 @pytest.mark.timeout(420)
-def test_config4_1M_ballots_100_selections_full_pipeline(group):
+def test_config4_1M_ballots_100_selections_full_pipeline(group, capsys):
     """configs[4] at N = 1: 1M ballots x 20 x (5+1), encrypt -> verify + tally -> fold ->
     5 trustees (quorum 3, 2 missing) -> exact counts; 200 spoiled ballots decrypted one by one."""
-    _full_pipeline_1M(group, 20, 4, nspoiled=200)
+    _full_pipeline_1M(group, 20, 4, nspoiled=200, say=_say(capsys))
 
 
 @pytest.mark.timeout(180)
-def test_config2_1M_ballots_4x5_full_pipeline(group):
+def test_config2_1M_ballots_4x5_full_pipeline(group, capsys):
     """configs[2]'s 1M ballots of 4 x (5+1) on one GPU as its 8 ranks shard them; 1,000 spoiled."""
-    _full_pipeline_1M(group, 4, 2, nspoiled=1000)
+    _full_pipeline_1M(group, 4, 2, nspoiled=1000, say=_say(capsys))
