@@ -6,8 +6,9 @@
 // integers mod p, i.e. identical to java.math.BigInteger.modPow / multiply+mod.
 //
 // Representation (MI355X-first):
-//   * radix 2^29, N = 144 limbs (4176 bits), Montgomery R = 2^4176 > 4p, so the
-//     CIOS loop never needs a final subtraction (values stay < 2p between ops);
+//   * radix 2^29, N = 144 limbs (4176 bits) per element, Montgomery R = 2^(29 * 142) = 2^4118 > 4p
+//     (142 CIOS steps: kSteps below), so the CIOS loop never needs a final subtraction (values stay
+//     < 2p between ops);
 //     (EG_RADIX=27 keeps the first design: N = 152, R = 2^4104);
 //   * every accumulator register takes ONE v_mad_u64_u32 per limb product with no
 //     carry-out handling: a register enters its lane's top position with a 29-bit limb,
@@ -26,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #ifndef EG_T
 #define EG_T 8
 #endif
@@ -37,7 +40,7 @@ namespace eg {
 #endif
 constexpr int kLimbBits = EG_RADIX;
 constexpr uint32_t kMask = (1u << kLimbBits) - 1u;
-constexpr int kN = EG_RADIX == 29 ? 144 : (EG_RADIX == 28 ? 148 : 152);  // limbs per element (R = 2^(kN*kLimbBits) > 4p)
+constexpr int kN = EG_RADIX == 29 ? 144 : (EG_RADIX == 28 ? 148 : 152);  // limbs per element (the layout; R: kSteps)
 constexpr int kT = EG_T;              // lanes per element
 constexpr int kL = kN / kT;           // limbs per lane
 constexpr int kLP = (kL + 3) & ~3;    // padded limbs per lane (16-B aligned lane blocks)
@@ -47,7 +50,21 @@ constexpr int kWave = 64;
 constexpr int kGroupsPerWave = kWave / kT;
 static_assert(kN % kT == 0, "limbs must split evenly over the group");
 static_assert(EG_RADIX >= 27 && EG_RADIX <= 29, "radix 2^27 (152 limbs), 2^28 (148) or 2^29 (144 limbs)");
-static_assert(kN * kLimbBits >= 4098, "R must exceed 4p (lazy reduction: values stay < 2p)");
+static_assert(kN * kLimbBits >= 4098, "the element format must hold values < 2p");
+// CIOS steps per Montgomery operation: the fewest radix-2^b digits whose R = 2^(b * steps) exceeds 4p
+// (p < 2^4096, values < 2p), 142 at radix 2^29, against the 144 limbs the 8-lane layout holds.  An
+// operand's limbs 142 and 143 are always zero (< 2p < 2^4097 = bit 4118 and above clear), so the two
+// steps whose multiplier digits they would be only run the m * p half; stopping after 142 steps is
+// Montgomery's multiply for R = 2^4118 (eg_capi.hip sets R mod p and R^2 mod p to match).  The last
+// trip stops kSkip steps early and the result sits in the accumulator at rotation kRot.
+#ifndef EG_CIOS_FULL
+#define EG_CIOS_FULL 0  // 1: all kN steps (R = 2^(kN * b), rounds 1-5's domain; A/B builds only)
+#endif
+constexpr int kSteps = EG_CIOS_FULL ? kN : (4098 + kLimbBits - 1) / kLimbBits;
+constexpr int kSkip = kN - kSteps;
+static_assert(kSteps * kLimbBits >= 4098, "R must exceed 4p (lazy reduction: values stay < 2p)");
+static_assert(kSkip >= 0 && kSkip < kL, "the skipped steps fit in the last trip");
+constexpr int kRot = (kL - kSkip) % kL;  // accumulator rotation after kSteps steps
 // Accumulator headroom: a register lives L steps in its lane and takes <= 2 products per step
 // (x*y + m*p; with SQR one doubled x*x product + m*p).  Radix 2^29 needs L <= 18.
 static_assert((unsigned __int128)2 * kL * (((1ull << kLimbBits) + 64) * ((1ull << kLimbBits) + 64)) < ((unsigned __int128)1 << 64), "radix 2^29 overflows the 64-bit columns above 18 limbs per lane");
@@ -158,6 +175,17 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t v) {
   return __builtin_amdgcn_mov_dpp(v, 0x111 /*row_shr:1*/, 0xF, 0xF, true);
 }
 
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): compile-time rotation indices
+template <int I, int N, class F>
+__device__ __forceinline__ void rsteps_from(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    rsteps_from<I + 1, N>(f);
+  }
+}
+template <int N, class F>
+__device__ __forceinline__ void rsteps(F& f) { rsteps_from<0, N>(f); }
+
 // Montgomery multiply  x <- x * y * R^-1 mod p  (result < 2p, limbs < 2^b + 2^(64-2b)+1).
 //   x : this lane's L limbs (in/out), any value < 2p, limbs <= 2^b + 2^(64-2b) + 1
 //   y : the group's LDS slot (kW words, device element format), value < 2p
@@ -242,8 +270,11 @@ __device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t*
   // the first step runs peeled (no accumulator zeroing); every trip s then runs its steps
   // 1..L-1 and the next trip's step 0 (same register rotation: r = 0 follows r = L-1)
   cios_step<FRIENDLY, SQR, true>(acc, x, 0, y[0], p, n0, mask, doff, dwid);
+  // full trips in the loop (each a whole register rotation, so the loop carries no register moves);
+  // with kSkip > 0 the last trip is straight-line code after it that stops after step kSteps - 1
+  constexpr int kFull = kSkip ? kT - 1 : kT;
 #pragma unroll 1
-  for (int s = 0; s < kT; ++s) {
+  for (int s = 0; s < kFull; ++s) {
     const uint32_t* ys = y + s * kLP;
 #pragma unroll
     for (int r = 1; r < kL; ++r) cios_step<FRIENDLY, SQR, false>(acc, x, r, ys[r], p, n0, mask, doff, dwid);
@@ -255,15 +286,22 @@ __device__ __forceinline__ void mont_mul_impl(uint32_t (&x)[kL], const uint32_t*
       cios_step<FRIENDLY, SQR, false>(acc, x, 0, ys[kLP], p, n0, mask, doff, dwid);
     }
   }
-  // two parallel carry passes -> limbs < 2^27 + 2^11 (enough headroom for the next op)
+  if constexpr (kSkip > 0) {  // the last trip (its step 0 ran at the end of the loop)
+    const uint32_t* ys = y + (kT - 1) * kLP;
+#pragma unroll
+    for (int r = 1; r < kL - kSkip; ++r) cios_step<FRIENDLY, SQR, false>(acc, x, r, ys[r], p, n0, mask, doff, dwid);
+  }
+  // two parallel carry passes -> limbs < 2^27 + 2^11 (enough headroom for the next op); limb j of the
+  // result is accumulator register (kRot + j) % kL
   uint64_t d[kL];
   {
-    uint64_t c_in = ((uint64_t)from_prev((uint32_t)(acc[kL - 1] >> kLimbBits)) |
-                     ((uint64_t)from_prev((uint32_t)(acc[kL - 1] >> (kLimbBits + 32))) << 32));
+    const uint64_t top = acc[(kRot + kL - 1) % kL];
+    uint64_t c_in = ((uint64_t)from_prev((uint32_t)(top >> kLimbBits)) |
+                     ((uint64_t)from_prev((uint32_t)(top >> (kLimbBits + 32))) << 32));
 #pragma unroll
     for (int j = 0; j < kL; ++j) {
-      const uint64_t c = (j == 0) ? c_in : (acc[j - 1] >> kLimbBits);
-      d[j] = (uint64_t)((uint32_t)acc[j] & mask) + c;
+      const uint64_t c = (j == 0) ? c_in : (acc[(kRot + j - 1) % kL] >> kLimbBits);
+      d[j] = (uint64_t)((uint32_t)acc[(kRot + j) % kL] & mask) + c;
     }
   }
   {
@@ -285,31 +323,37 @@ __device__ __forceinline__ void mont_redc_impl(uint32_t (&x)[kL], const PT& p, u
   uint64_t acc[kL];
 #pragma unroll
   for (int j = 0; j < kL; ++j) acc[j] = x[j];
-#pragma unroll 1
-  for (int s = 0; s < kT; ++s) {
-#pragma unroll
-    for (int r = 0; r < kL; ++r) {
-      uint32_t t0 = (uint32_t)acc[r % kL];
-      if constexpr (!FRIENDLY) t0 *= n0;
-      const uint32_t m = bcast_g0_and(t0, mask);
-#pragma unroll
-      for (int j = 0; j < kL; ++j) {
-        uint64_t& A = acc[(j + r) % kL];
-        A = (uint64_t)p[j] * m + A;
-      }
-      uint64_t& A0 = acc[r % kL];
-      acc[(r + 1) % kL] += A0 >> kLimbBits;
-      A0 = (uint64_t)from_next_and((uint32_t)A0, mask);
-    }
-  }
-  uint64_t d[kL];
-  {
-    uint64_t c_in = ((uint64_t)from_prev((uint32_t)(acc[kL - 1] >> kLimbBits)) |
-                     ((uint64_t)from_prev((uint32_t)(acc[kL - 1] >> (kLimbBits + 32))) << 32));
+  // one reduction step at rotation r (compile-time)
+  auto rstep = [&](auto R) {
+    constexpr int r = decltype(R)::value;
+    uint32_t t0 = (uint32_t)acc[r % kL];
+    if constexpr (!FRIENDLY) t0 *= n0;
+    const uint32_t m = bcast_g0_and(t0, mask);
 #pragma unroll
     for (int j = 0; j < kL; ++j) {
-      const uint64_t c = (j == 0) ? c_in : (acc[j - 1] >> kLimbBits);
-      d[j] = (uint64_t)((uint32_t)acc[j] & mask) + c;
+      uint64_t& A = acc[(j + r) % kL];
+      A = (uint64_t)p[j] * m + A;
+    }
+    uint64_t& A0 = acc[r % kL];
+    acc[(r + 1) % kL] += A0 >> kLimbBits;
+    A0 = (uint64_t)from_next_and((uint32_t)A0, mask);
+  };
+  // kSteps steps (R = 2^(b * kSteps)): full trips in the loop, then the last trip's first kL - kSkip
+  constexpr int kFull = kSkip ? kT - 1 : kT;
+#pragma unroll 1
+  for (int s = 0; s < kFull; ++s) {
+    rsteps<kL>(rstep);
+  }
+  if constexpr (kSkip > 0) rsteps<kL - kSkip>(rstep);
+  uint64_t d[kL];
+  {
+    const uint64_t top = acc[(kRot + kL - 1) % kL];
+    uint64_t c_in = ((uint64_t)from_prev((uint32_t)(top >> kLimbBits)) |
+                     ((uint64_t)from_prev((uint32_t)(top >> (kLimbBits + 32))) << 32));
+#pragma unroll
+    for (int j = 0; j < kL; ++j) {
+      const uint64_t c = (j == 0) ? c_in : (acc[(kRot + j - 1) % kL] >> kLimbBits);
+      d[j] = (uint64_t)((uint32_t)acc[(kRot + j) % kL] & mask) + c;
     }
   }
   {

@@ -716,14 +716,14 @@ extern "C" int eg_ctx_create(const uint8_t p_be[512], const uint8_t q_be[32], co
   std::memcpy(c->p_be, p_be, 512);
   std::memcpy(c->q_be, q_be, 32);
   std::memcpy(c->g_be, g_be, 512);
-  // Montgomery constants, R = 2^(kLimbBits*kN)
+  // Montgomery constants, R = 2^(kLimbBits * kSteps) (eg_bignum.hpp: 2^4118 at radix 2^29)
   Big P1 = p;
   P1.push_back(0);  // room for doubling
   Big r(129, 0);
   r[0] = 1;
-  for (int i = 0; i < kN * kLimbBits; ++i) dbl_mod(r, P1);  // R mod p
+  for (int i = 0; i < kSteps * kLimbBits; ++i) dbl_mod(r, P1);  // R mod p
   Big r2 = r;
-  for (int i = 0; i < kN * kLimbBits; ++i) dbl_mod(r2, P1);  // R^2 mod p
+  for (int i = 0; i < kSteps * kLimbBits; ++i) dbl_mod(r2, P1);  // R^2 mod p
   words_to_elem(p, c->h.p);
   words_to_elem(r2, c->h.r2);
   words_to_elem(r, c->h.one);

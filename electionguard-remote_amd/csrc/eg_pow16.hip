@@ -14,6 +14,7 @@
 #pragma clang diagnostic ignored "-Wunused-value"
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "eg_pow16.h"
@@ -140,6 +141,11 @@ namespace egw {
 constexpr int kBits = 29, kLimbs = 144, kLL = 3, kLanes = 48, kRow = 64 * kLL;
 constexpr uint32_t kM = (1u << kBits) - 1u;
 static_assert(kLanes * kLL == kLimbs, "48 lanes x 3 limbs");
+// the Montgomery domain of eg_bignum.hpp (R = 2^(29 * kSteps), 142 steps): limbs 142 and 143 of every
+// operand are zero, so the multiply stops two steps early; the result then sits at rotation kRot
+constexpr int kSteps = eg16::kSteps, kSkip = kLimbs - kSteps, kRot = kSteps % kLL;
+constexpr int kTrips = kSteps / kLL, kRem = kSteps % kLL;  // 47 full trips of 3 steps + 1 step
+static_assert(kSkip >= 0 && kSkip < kLL && kSteps * kBits >= 4098, "Montgomery R must exceed 4p");
 
 struct Consts {
   uint32_t p[kRow], r2[kRow], one[kRow];  // limb i at [i], zeros from 144 on
@@ -153,15 +159,17 @@ __device__ __forceinline__ uint32_t lane64() { return __builtin_amdgcn_mbcnt_hi(
 __device__ __forceinline__ uint32_t wnext(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x130 /*wave_shl:1*/, 0xF, 0xF, true); }
 __device__ __forceinline__ uint32_t wprev(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x138 /*wave_shr:1*/, 0xF, 0xF, true); }
 
-// x <- x * y * R^-1 mod p (R = 2^4176), result < 2p with limbs < 2^29 + small; y may alias x
+// x <- x * y * R^-1 mod p (R = 2^4118: kSteps = 142 steps), result < 2p with limbs < 2^29 + small; y may alias x
 template <bool F>
 __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL], const uint32_t (&p)[kLL], uint32_t n0,
                                     uint32_t mv) {
   uint64_t acc[kLL] = {0, 0, 0};
-#pragma unroll 1
-  for (int q = 0; q < kLanes; ++q) {  // multiplier limbs 3q .. 3q+2 live in lane q
+  // kSteps steps: full trips in the loop (multiplier limbs 3q .. 3q+2 live in lane q), then the last
+  // trip's first kLL - kSkip steps
+  auto trip = [&](const int q, auto NR) {
+    constexpr int nr = decltype(NR)::value;
 #pragma unroll
-    for (int r = 0; r < kLL; ++r) {
+    for (int r = 0; r < nr; ++r) {
       const uint32_t yi = __builtin_amdgcn_readlane(y[r], q);
 #pragma unroll
       for (int j = 0; j < kLL; ++j) {
@@ -180,14 +188,19 @@ __device__ __forceinline__ void mul(uint32_t (&x)[kLL], const uint32_t (&y)[kLL]
       acc[(r + 1) % kLL] += A0 >> kBits;         // the carry stays in this lane's next column
       A0 = (uint64_t)(wnext((uint32_t)A0) & mv);  // the low bits move to the lane below's top column
     }
-  }
-  // two carry passes (the registers are back in natural order: 144 steps = 48 x 3)
+  };
+  constexpr int kFullTrips = kSkip ? kLanes - 1 : kLanes;
+#pragma unroll 1
+  for (int q = 0; q < kFullTrips; ++q) trip(q, std::integral_constant<int, kLL>{});
+  if constexpr (kSkip > 0) trip(kLanes - 1, std::integral_constant<int, kLL - kSkip>{});
+  // two carry passes (limb j of the result is register (kRot + j) % 3: 142 steps = 47 x 3 + 1)
   uint64_t d[kLL];
   {
-    const uint64_t top = acc[kLL - 1] >> kBits;
+    const uint64_t top = acc[(kRot + kLL - 1) % kLL] >> kBits;
     const uint64_t c_in = (uint64_t)wprev((uint32_t)top) | ((uint64_t)wprev((uint32_t)(top >> 32)) << 32);
 #pragma unroll
-    for (int j = 0; j < kLL; ++j) d[j] = (uint64_t)((uint32_t)acc[j] & kM) + (j == 0 ? c_in : (acc[j - 1] >> kBits));
+    for (int j = 0; j < kLL; ++j)
+      d[j] = (uint64_t)((uint32_t)acc[(kRot + j) % kLL] & kM) + (j == 0 ? c_in : (acc[(kRot + j - 1) % kLL] >> kBits));
   }
   const uint32_t c_in = wprev((uint32_t)(d[kLL - 1] >> kBits));
 #pragma unroll
@@ -215,37 +228,40 @@ __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[k
   __builtin_amdgcn_wave_barrier();
   uint64_t acc[kLL] = {0, 0, 0};
   uint32_t m1 = 0, m2 = 0;  // quotient digits of the previous two steps
+  // one CIOS step at rotation R (a compile-time constant) with multiplier digit yi
+  auto step = [&](auto R, const uint32_t yi) {
+    constexpr int r = decltype(R)::value;
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) {
+      uint64_t& A = acc[(j + r) % kLL];
+      A = (uint64_t)x[j] * yi + A;
+    }
+    // keep one v_mad_u64_u32 per product: without the barrier the compiler re-associates the
+    // early-known m2 terms into separate products plus 64-bit adds (r04h: 25% slower)
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) asm volatile("" : "+v"(acc[j]));
+    asm volatile("" : "+s"(m2));  // a 32-bit SGPR: otherwise the loop carries it widened to 64 bits (two MACs)
+#pragma unroll
+    for (int j = 0; j < kLL; ++j) {
+      uint64_t& A = acc[(j + r) % kLL];
+      A = (uint64_t)pd[j] * m2 + A;
+    }
+    uint64_t& A0 = acc[r];
+    const uint32_t m = __builtin_amdgcn_readlane((uint32_t)A0, 0) & kM;
+    acc[(r + 1) % kLL] += A0 >> kBits;
+    A0 = (uint64_t)(wnext((uint32_t)A0) & mv);
+    m2 = m1;
+    m1 = m;
+  };
   // three CIOS steps with the multiplier digits yc (limbs 3q .. 3q + 2)
   auto steps = [&](const uint32_t (&yc)[kLL]) {
-#pragma unroll
-    for (int r = 0; r < kLL; ++r) {
-      const uint32_t yi = yc[r];
-#pragma unroll
-      for (int j = 0; j < kLL; ++j) {
-        uint64_t& A = acc[(j + r) % kLL];
-        A = (uint64_t)x[j] * yi + A;
-      }
-      // keep one v_mad_u64_u32 per product: without the barrier the compiler re-associates the
-      // early-known m2 terms into separate products plus 64-bit adds (r04h: 25% slower)
-#pragma unroll
-      for (int j = 0; j < kLL; ++j) asm volatile("" : "+v"(acc[j]));
-      asm volatile("" : "+s"(m2));  // a 32-bit SGPR: otherwise the loop carries it widened to 64 bits (two MACs)
-#pragma unroll
-      for (int j = 0; j < kLL; ++j) {
-        uint64_t& A = acc[(j + r) % kLL];
-        A = (uint64_t)pd[j] * m2 + A;
-      }
-      uint64_t& A0 = acc[r];
-      const uint32_t m = __builtin_amdgcn_readlane((uint32_t)A0, 0) & kM;
-      acc[(r + 1) % kLL] += A0 >> kBits;
-      A0 = (uint64_t)(wnext((uint32_t)A0) & mv);
-      m2 = m1;
-      m1 = m;
-    }
+    step(std::integral_constant<int, 0>{}, yc[0]);
+    step(std::integral_constant<int, 1>{}, yc[1]);
+    step(std::integral_constant<int, 2>{}, yc[2]);
   };
   uint32_t ya[kLL] = {yb[0], yb[1], yb[2]}, yz[kLL];
 #pragma unroll 1
-  for (int q = 0; q < kLanes; q += 2) {
+  for (int q = 0; q + 1 < kTrips; q += 2) {
     const uint32_t* yq = yb + kLL * q;
 #pragma unroll
     for (int r = 0; r < kLL; ++r) yz[r] = yq[kLL + r];  // trip q + 1's digits
@@ -258,18 +274,22 @@ __device__ __forceinline__ void mul_d2(uint32_t (&x)[kLL], const uint32_t (&y)[k
     for (int r = 0; r < kLL; ++r) asm volatile("" : "+v"(yz[r]));
     steps(yz);
   }
-  // the last two digits: after 144 steps position P holds column 144 + P, m_142 * p~_J belongs to
-  // P = J - 2 (pd) and m_143 * p~_J to P = J - 1 (pd1)
+  if constexpr (kTrips % 2 == 1) steps(ya);  // the odd last full trip (trip 46: prefetched as "q + 2")
+  if constexpr (kRem >= 1) step(std::integral_constant<int, 0>{}, yb[kLL * kTrips]);  // step 141
+  if constexpr (kRem >= 2) step(std::integral_constant<int, 1>{}, yb[kLL * kTrips + 1]);
+  // the last two digits: after kSteps steps position P (register (kRot + P) % 3 of its lane) holds
+  // column kSteps + P; m_{kSteps-2} * p~_J belongs to P = J - 2 (pd) and m_{kSteps-1} * p~_J to P = J - 1 (pd1)
 #pragma unroll
-  for (int j = 0; j < kLL; ++j) acc[j] = (uint64_t)pd[j] * m2 + acc[j];
+  for (int j = 0; j < kLL; ++j) acc[(kRot + j) % kLL] = (uint64_t)pd[j] * m2 + acc[(kRot + j) % kLL];
 #pragma unroll
-  for (int j = 0; j < kLL; ++j) acc[j] = (uint64_t)pd1[j] * m1 + acc[j];
+  for (int j = 0; j < kLL; ++j) acc[(kRot + j) % kLL] = (uint64_t)pd1[j] * m1 + acc[(kRot + j) % kLL];
   uint64_t d[kLL];
   {
-    const uint64_t top = acc[kLL - 1] >> kBits;
+    const uint64_t top = acc[(kRot + kLL - 1) % kLL] >> kBits;
     const uint64_t c_in = (uint64_t)wprev((uint32_t)top) | ((uint64_t)wprev((uint32_t)(top >> 32)) << 32);
 #pragma unroll
-    for (int j = 0; j < kLL; ++j) d[j] = (uint64_t)((uint32_t)acc[j] & kM) + (j == 0 ? c_in : (acc[j - 1] >> kBits));
+    for (int j = 0; j < kLL; ++j)
+      d[j] = (uint64_t)((uint32_t)acc[(kRot + j) % kLL] & kM) + (j == 0 ? c_in : (acc[(kRot + j - 1) % kLL] >> kBits));
   }
   const uint32_t c_in = wprev((uint32_t)(d[kLL - 1] >> kBits));
 #pragma unroll

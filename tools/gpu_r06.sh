@@ -58,3 +58,10 @@ fi
 if [[ $STEPS == *prof* ]]; then
   bash tools/profile_round.sh ${TAG}
 fi
+if [[ $STEPS == *ab142* ]]; then
+  # 142 CIOS steps (R = 2^4118, the default) against all 144 (EG_CIOS_FULL=1), per shader clock, three
+  # interleaved rounds of the configs[1] verify
+  AB_MODE=verify AB_NB=10000 AB_WB=22 timeout -k 10 900 python tools/ab_mm.py s142= s144=-DEG_CIOS_FULL=1 s142= \
+    s144=-DEG_CIOS_FULL=1 s142= s144=-DEG_CIOS_FULL=1 > gpurun_out/${TAG}_ab_steps.log 2>&1
+  echo "ab142: $(tail -c 900 gpurun_out/${TAG}_ab_steps.log)"
+fi
