@@ -1,7 +1,7 @@
 // eg_pow16.hip — the latency-shaped instantiation of the device core: the same kernels as the
 // throughput path (eg_kernels.hpp: k_import, the op-program k_pow, k_export) compiled with 16 lanes
 // per element (EG_T = 16) in namespace eg16.  A 4096-bit exponentiation is ~330 Montgomery
-// operations in sequence; an 8-lane group runs each in ~12 us (L = 18 limbs per lane: 144 CIOS
+// operations in sequence; an 8-lane group runs each in ~12 us (L = 18 limbs per lane: 142 CIOS
 // steps of 36 MACs + glue), a 16-lane group in about half (L = 9, and the quotient broadcast is one
 // row_newbcast move), so a batch that fits one resident round finishes in about half the time.
 // That is what a blocking per-element caller waits for (eg_capi_coalesce.inc); large batches keep
