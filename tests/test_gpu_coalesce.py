@@ -128,9 +128,8 @@ def test_constant_time_mode_recorded_per_job(group, oracle_group):
     og = oracle_group
     rng = random.Random(5150)
     subs = []
-    group.set_coalescing(16384, 30000)
+    group.set_coalescing(16384, 30000)  # the next batch waits for 16384 jobs or the fixed 30 ms window
     try:
-        group.multP_one(1, 1)  # the previous dispatch took one job
         group.ct_pow = True
         for i in range(6):  # secret-exponent jobs: g^x and b^x
             x = rng.randrange(og.q)

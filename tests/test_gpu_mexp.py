@@ -212,9 +212,10 @@ def test_table_destroyed_with_jobs_queued(group, oracle_group):
     fb = group.fixed_base(K, 8)
     es = [rng.randrange(og.q) for _ in range(40)]
     import time
-    group.set_coalescing(4096, 20000)  # a FIXED 20 ms window (honoured exactly): still queued at the close
+    # a FIXED 20 ms window (honoured exactly), and eg_ctx_set_coalescing makes the next batch wait for
+    # max_batch jobs or the window: the 40 jobs are still queued at the close
+    group.set_coalescing(4096, 20000)
     try:
-        group.multP_one(1, 1)  # the previous dispatch took 1 job: 40 jobs do not end the window early
         t = time.monotonic()
         ts = [group.mexp_submit([], None, [(fb, e)]) for e in es]
         fb.close()
