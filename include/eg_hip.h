@@ -311,7 +311,13 @@ int eg_all_nonzero_dev(eg_ctx* ctx, const uint8_t* d_flags, size_t n, int* all);
  * eg_tally_allgather_fold: every rank passes nparts partial tallies of n elements (d_parts_be,
  * nparts x n x 512 B big-endian in HBM); root receives out_be[k] = product over every rank and
  * part of element k mod p (n x 512 B, host; may be NULL on the other ranks).  One ncclAllGather
- * plus the k_prod tree on root's GPU.  Without eg_comm_init it folds the local parts alone. */
+ * plus the k_prod tree on root's GPU.  Without eg_comm_init it folds the local parts alone.
+ * Deadlines: the communicator is non-blocking; eg_comm_init, every collective's enqueue AND its
+ * completion (a hipEvent behind it, polled with ncclCommGetAsyncError) wait at most EG_COMM_TIMEOUT_S
+ * seconds (default 300).  On expiry or an asynchronous error the communicator is aborted
+ * (ncclCommAbort), the call returns EG_ERR_HIP, and the context stays FAILED: eg_comm_all_valid and
+ * eg_tally_allgather_fold then return EG_ERR_STATE (never a fold of the local parts alone) until
+ * eg_comm_destroy or eg_comm_init resets it. */
 #define EG_COMM_ID_BYTES 128
 int eg_comm_unique_id(uint8_t id[EG_COMM_ID_BYTES]);
 int eg_comm_init(eg_ctx* ctx, const uint8_t id[EG_COMM_ID_BYTES], int world, int rank);
