@@ -18,6 +18,6 @@ def test_collective_wait_with_fake_communicators(tmp_path):
     res = json.loads(r.stdout)
     assert r.returncode == 0 and res["failures"] == 0, res
     nc = res["never_completes"]
-    assert nc["result"] == "timed out" and 0.4 <= nc["seconds"] < 0.9
+    assert nc["result"] == "timed out" and 0.4 <= nc["seconds"] < 3.0
     assert res["async_error"]["result"] == "communicator error" and res["async_error"]["code"] == 6
     assert res["completes"]["result"] == "done" and res["stream_error"]["result"] == "stream error"
