@@ -171,8 +171,11 @@ def init_ranks(a):
     world = lw or 1
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if exchange_mode() == "gloo":
-        local = 0  # the rehearsal puts every rank on one GPU
+    if exchange_mode() == "gloo" or os.environ.get("EG_RANKS_SHARE_GPU") == "1":
+        # the gloo rehearsal puts every rank on one GPU; EG_RANKS_SHARE_GPU=1 does the same in RCCL
+        # mode, where RCCL refuses two ranks on one device: the failure path of --strict-rccl on a
+        # one-GPU box (every rank must exit non-zero within seconds, none may hang)
+        local = 0
     dist = None
     if world > 1:
         import datetime
