@@ -69,10 +69,12 @@ if [[ $STEPS == *strictfail* ]]; then
   # --strict-rccl against a real RCCL refusal: 2 ranks on one device (EG_RANKS_SHARE_GPU=1); the run must
   # fail (non-zero) on every rank, quickly, with no host-exchange line
   set +e
-  /usr/bin/time -f "wall %e s" timeout -k 10 300 env EG_RANKS_SHARE_GPU=1 python bench.py --gpus 2 --steps 1 --warmup 1 \
+  t0=$SECONDS
+  timeout -k 10 300 env EG_RANKS_SHARE_GPU=1 python bench.py --gpus 2 --steps 1 --warmup 1 \
     --ballots 2000 --fb-window 12 --cpu-sample 0 --modexp-n 0 --ct-encrypt 0 > gpurun_out/${TAG}_strict_fail.log 2>&1
   rc=$?
   set -e
-  echo "strictfail: rc=$rc $(tail -c 600 gpurun_out/${TAG}_strict_fail.log)"
-  [[ $rc -ne 0 && $rc -ne 124 && $rc -ne 137 ]]
+  echo "exit status $rc after $((SECONDS - t0)) s" >> gpurun_out/${TAG}_strict_fail.log
+  echo "strictfail: rc=$rc $(tail -c 800 gpurun_out/${TAG}_strict_fail.log)"
+  [[ $rc -ne 0 && $rc -ne 124 && $rc -ne 137 && $rc -ne 127 ]]
 fi
