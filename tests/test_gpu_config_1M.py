@@ -19,7 +19,9 @@ laid out by hand).  The CPU oracle cannot redo 1M ballots in a test's time, so p
 size-independent properties: every verdict valid, the fold equal to the sequential product of the
 shard tallies, the decrypted counts EXACTLY the plaintext vote sums over the cast ballots, every
 decryption-record check (share proofs, recovery keys, quorum, B = M g^t), and every spoiled
-ballot decrypting to its own votes.  (The oracle pins the same kernels at small sizes:
+ballot decrypting to its own votes; in the 4 x (5+1) run, three records of the last shard tampered
+(a range-proof response, a contest challenge, a non-residue pad) flip exactly their verdicts on
+a re-verify of all 125,000 ballots.  (The oracle pins the same kernels at small sizes:
 test_gpu_golden.py, test_gpu_benchconfig.py, test_gpu_fullsize.py.)
 
 Host nonce generation for shard k+1 overlaps the GPU's work on shard k (ctypes releases the GIL).
@@ -43,7 +45,37 @@ def _shard_inputs(seed, k, man, q):
     return votes, random_scalars(rng, (SHARD, man.nsel, 4), q), random_scalars(rng, (SHARD, man.n_contests), q)
 
 
-def _full_pipeline_1M(group, contests, seed, nspoiled, say=print):
+def _tamper_last_shard(group, man, ver, cts, rp, cp, oks, okc, tal):
+    """Full-size tamper detection on the last shard (125,000 ballots, re-verified on the device):
+    one selection's range-proof response, one contest proof's challenge, and one ciphertext's pad
+    multiplied by p - 1 (an element with an order-2 component: not a residue, so its range proof, its
+    residue test and its contest's aggregate all fail).  Exactly these verdicts flip; every other of
+    the shard's flags stays valid."""
+    b1, s1 = 12_345, 3
+    b2, c2 = 54_321, man.n_contests - 1
+    b3, s3 = 99_999, man.spc + 1  # a selection of contest 1
+    r = rp[b1:b1 + 1].download()
+    r[0, s1, 1, 31] ^= 1
+    rp[b1:b1 + 1].upload(r)
+    c = cp[b2:b2 + 1].download()
+    c[0, c2, 0, 5] ^= 0x40
+    cp[b2:b2 + 1].upload(c)
+    e = cts[b3:b3 + 1].download()
+    alpha = int.from_bytes(e[0, s3, 0].tobytes(), "big")
+    e[0, s3, 0] = np.frombuffer((alpha * (group.p - 1) % group.p).to_bytes(512, "big"), np.uint8)
+    cts[b3:b3 + 1].upload(e)
+    oks.zero()
+    okc.zero()
+    ver.verify_device(cts.ptr, rp.ptr, cp.ptr, SHARD, oks.ptr, okc.ptr, tal.ptr)
+    group.sync()
+    fs, fc = oks.download().reshape(SHARD, man.nsel), okc.download().reshape(SHARD, man.n_contests)
+    bad_s = {tuple(x) for x in np.argwhere(fs == 0)}
+    bad_c = {tuple(x) for x in np.argwhere(fc == 0)}
+    assert bad_s == {(b1, s1), (b3, s3)}, bad_s
+    assert bad_c == {(b2, c2), (b3, s3 // man.spc)}, bad_c
+
+
+def _full_pipeline_1M(group, contests, seed, nspoiled, say=print, tamper=False):
     from electionguard.ballot import ElectionKey, Manifest, Verifier, batch_encryption_device
     from electionguard.decrypt import Decryption, DecryptingTrustee, verify_decryption_record
     from electionguard.keyceremony import key_ceremony, verify_backups, verify_commitment_proofs
@@ -104,6 +136,9 @@ def _full_pipeline_1M(group, contests, seed, nspoiled, say=print):
                 spoiled_cts = cts[0:nspoiled].download()
                 spoiled_votes = real[:nspoiled]
             say(f"  shard {k + 1}/{SHARDS}: {(k + 1) * SHARD} ballots, encrypt {t_enc:.1f} s, verify+tally {t_ver:.1f} s")
+    if tamper:  # (the last shard's tally is already in parts)
+        _tamper_last_shard(group, man, ver, cts, rp, cp, oks, okc, tal)
+        say("  tampered last shard: exactly the 4 expected verdicts flipped")
     del cts, rp, cp, dsn, dcn, dv, oks, okc
     # rank 0's fold after the all-gather: parts laid out (world, n_real * 2, 512) as ncclAllGather leaves them
     gathered = np.ascontiguousarray(np.stack(parts)).reshape(SHARDS, man.n_real * 2, 512)
@@ -153,5 +188,6 @@ def test_config4_1M_ballots_100_selections_full_pipeline(group, capsys):
 
 @pytest.mark.timeout(180)
 def test_config2_1M_ballots_4x5_full_pipeline(group, capsys):
-    """configs[2]'s 1M ballots of 4 x (5+1) on one GPU as its 8 ranks shard them; 1,000 spoiled."""
-    _full_pipeline_1M(group, 4, 2, nspoiled=1000, say=_say(capsys))
+    """configs[2]'s 1M ballots of 4 x (5+1) on one GPU as its 8 ranks shard them; 1,000 spoiled; and
+    three tampered records in the last 125,000-ballot shard flip exactly their verdicts."""
+    _full_pipeline_1M(group, 4, 2, nspoiled=1000, say=_say(capsys), tamper=True)
